@@ -1,0 +1,89 @@
+"""Backward host launcher: same contract as /root/reference/src/backward/caller.py:14-178.
+
+`_flash_attn_backward(dO, q, k, v, bias, attention_mask, o, lse, dropout_p, causal,
+softmax_scale, dropout_seed) -> (dq, dk, dv)`.  The reference's three steps -- Triton
+_compute_delta (:95-114), Triton _bwd_kernel (:122-160) and the host GQA sum of dK/dV over
+the q-heads of each group (:162-165) -- become one call of the C ABI `fa2_bwd`, which runs
+delta, dK/dV (fp32 group sum in registers) and dQ kernels on the current stream.  dQ is
+produced in q.dtype directly (the reference accumulates a fp32 buffer that autograd then casts,
+:86); dK/dV come out with Hkv heads.  Varlen rows are handled in place (no trim / pack /
+unpack, :29-79, :167-176).
+"""
+import ctypes
+import math
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, stream_of
+
+
+def _flash_attn_backward(
+    dO: Tensor,
+    q: Tensor,
+    k: Tensor,
+    v: Tensor,
+    bias: Optional[Tensor],
+    attention_mask: Optional[Tensor],
+    o: Tensor,
+    lse: Tensor,
+    dropout_p: float,
+    causal: bool,
+    softmax_scale: Optional[float],
+    dropout_seed: Optional[int],
+    dq_dtype: Optional[torch.dtype] = None,
+) -> Tuple[Tensor, Tensor, Tensor]:
+    if attention_mask is not None:
+        assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
+        assert q.size(1) == k.size(1), "Attention mask is not supported with seqlen_q != seqlen_k"
+    dO = dO if dO.stride(-1) == 1 else dO.contiguous()
+    batch, seqlen_q, nheads_q, head_dim = q.shape
+    _, seqlen_k, nheads_kv, _ = k.shape
+    lse_rows = math.ceil(seqlen_q / 128) * 128
+    softmax_scale = 1.0 / math.sqrt(head_dim) if softmax_scale is None else softmax_scale
+    assert nheads_q % nheads_kv == 0, f"{nheads_q = } is not divisible by {nheads_kv = }"
+    assert lse.shape == (batch, nheads_q, lse_rows) and lse.is_contiguous()
+    assert q.stride(-1) == k.stride(-1) == v.stride(-1) == o.stride(-1) == 1
+    assert dO.dtype == q.dtype == k.dtype == v.dtype == o.dtype
+
+    stride_bb, stride_bh, stride_bm = infer_bias_strides(bias, batch, nheads_q, seqlen_q, seqlen_k)
+    dropout_seed = handle_dropout(dropout_p, dropout_seed, is_forward=False)
+    cu_seqlens = cu_seqlens_from_mask(attention_mask) if attention_mask is not None else None
+
+    dq_dtype = q.dtype if dq_dtype is None else dq_dtype
+    dq = torch.empty(q.shape, dtype=dq_dtype, device=q.device)
+    dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+    dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+    delta = torch.empty_like(lse)
+
+    args = _lib.BwdArgs()
+    args.q, args.k, args.v, args.o, args.dout = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr()
+    args.lse, args.delta = lse.data_ptr(), delta.data_ptr()
+    args.dq, args.dk, args.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+    args.bias = bias.data_ptr() if bias is not None else None
+    args.cu_seqlens = cu_seqlens.data_ptr() if cu_seqlens is not None else None
+    args.q_stride[:] = bshd_strides(q)
+    args.k_stride[:] = bshd_strides(k)
+    args.v_stride[:] = bshd_strides(v)
+    args.o_stride[:] = bshd_strides(o)
+    args.do_stride[:] = bshd_strides(dO)
+    args.dq_stride[:] = bshd_strides(dq)
+    args.dk_stride[:] = bshd_strides(dk)
+    args.dv_stride[:] = bshd_strides(dv)
+    args.bias_stride[:] = (stride_bb, stride_bh, stride_bm)
+    args.batch, args.heads_q, args.heads_kv = batch, nheads_q, nheads_kv
+    args.seqlen_q, args.seqlen_k, args.head_dim = seqlen_q, seqlen_k, head_dim
+    args.lse_row_stride = lse_rows
+    args.causal = int(bool(causal))
+    args.dtype = encode_dtype(q)
+    args.bias_dtype = encode_dtype(bias) if bias is not None else 0
+    args.dq_dtype = encode_dtype(dq)
+    args.softmax_scale = float(softmax_scale)
+    args.dropout_p = float(dropout_p)
+    args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
+    lib = _lib.load()
+    with torch.cuda.device(q.device):
+        _lib.check(lib.fa2_bwd(ctypes.byref(args), stream_of(q)))
+    return dq, dk, dv

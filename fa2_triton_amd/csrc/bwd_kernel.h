@@ -1,0 +1,427 @@
+// bwd.hip -- FlashAttention-2 backward for gfx950 (CDNA4).
+//
+// Replaces the reference's backward launches (/root/reference/src/backward/caller.py:95-165):
+//   delta_kernel  <- _compute_delta        (/root/reference/src/backward/compute_delta.py:17-73)
+//   dkdv_kernel   <- _bwd_kernel, pid < NUM_BLOCKS_KV branch + the host GQA sum
+//                    (/root/reference/src/backward/kernel.py:154-166, compute_dkdv.py:7-296,
+//                     caller.py:162-165)
+//   dq_kernel     <- _bwd_kernel, dQ branch (kernel.py:168-182, compute_dq.py:7-261)
+// Same math (src/backward/compute_dkdv.py:89-110, compute_dq.py:70-76):
+//   P = exp2(s * scale * log2e - LSE2), dV = P^T dO, dP = dO V^T, dS = P (dP - delta) scale,
+//   dK = dS^T Q, dQ = dS K; P and dS rounded to the input dtype before their MFMAs; fp32
+//   accumulation; no atomics (bitwise reproducible, as tests/test_repeatability.py demands).
+// Differences by design: the GQA group sum of dK/dV is done in fp32 registers inside
+// dkdv_kernel (the reference sums bf16/fp16 tensors on the host), dQ is written directly in
+// the requested dtype, and padded varlen rows are handled in place (no pack/unpack).
+#include "common.h"
+#include "fa2_internal.h"
+
+namespace fa2 {
+
+// ---------------------------------------------------------------------------------------------
+// delta[b, h, i] = sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows)
+template <bool BF16, bool ALIGNED>
+__global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int LPR = 16;             // lanes per row
+  constexpr int ROWS = 256 / LPR;     // rows per block
+  const int tid = threadIdx.x;
+  const int row = blockIdx.x * ROWS + tid / LPR;
+  const int sub = tid % LPR;
+  const int bh = blockIdx.y;
+  const int b = bh / p.heads_q, h = bh - b * p.heads_q;
+  int Lq = p.seqlen_q;
+  if (p.cu_seqlens) Lq = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+  float acc = 0.f;
+  if (row < Lq) {
+    const uint16_t* orow = (const uint16_t*)p.o + b * p.o_stride[0] + h * p.o_stride[2] + (int64_t)row * p.o_stride[1];
+    const uint16_t* drow = (const uint16_t*)p.dout + b * p.do_stride[0] + h * p.do_stride[2] + (int64_t)row * p.do_stride[1];
+    for (int d0 = sub * 8; d0 < p.head_dim; d0 += LPR * 8) {
+      const u32x4 ov = load_row_frag<ALIGNED>(orow, d0, p.head_dim, true);
+      const u32x4 dv = load_row_frag<ALIGNED>(drow, d0, p.head_dim, true);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc += E::to_f32((uint16_t)(ov[j] & 0xFFFF)) * E::to_f32((uint16_t)(dv[j] & 0xFFFF));
+        acc += E::to_f32((uint16_t)(ov[j] >> 16)) * E::to_f32((uint16_t)(dv[j] >> 16));
+      }
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, LPR);
+  // rows [Lq, lse_row_stride) get 0 so that masked rows can never inject NaN/Inf garbage
+  if (sub == 0 && row < p.lse_row_stride) p.delta[(int64_t)bh * p.lse_row_stride + row] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK, dV: one workgroup = 4 waves = 128 keys of one (batch, kv-head); wave w owns keys
+// n0 + 32 w + (lane & 31).  K and V stay in VGPRs as the B operands of S = Q K^T and
+// dP = dO V^T; the workgroup sweeps the q-heads of its GQA group and 32-row query tiles
+// (Q and dO staged in LDS, double buffered).  Per tile and wave:
+//   S[q][key], dP[q][key]   8 + 8 MFMA (A = Q / dO row fragments from LDS)
+//   dV^T[d][key] += dO^T P  NDT*2 MFMA (A = dO^T via ds_read_b64_tr_b16, B = P registers)
+//   dK^T[d][key] += Q^T dS  NDT*2 MFMA
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
+__global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int NT = 256;
+  constexpr int BNK = 128;          // keys per workgroup
+  constexpr int BMQ = 32;           // query rows per tile
+  constexpr int KS = DT / 16;
+  constexpr int NDT = DT / 32;
+  constexpr int TILE = BMQ * DT * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // Q0 dO0 Q1 dO1
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int n0 = blockIdx.x * BNK;
+  const int bkv = blockIdx.y;
+  const int b = bkv / p.heads_kv, hkv = bkv - b * p.heads_kv;
+  const int G = p.heads_q / p.heads_kv;
+  int Lq = p.seqlen_q, Lk = p.seqlen_k;
+  if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+  const int D = p.head_dim;
+  const int diag = Lk - Lq;
+  const int kw0 = n0 + 32 * w;   // first key of this wave
+  const int kj = kw0 + r32;      // this lane's key
+  const float scale = p.softmax_scale, scale2 = scale * kLog2e;
+
+  // K / V fragments: B operands, K[kj][16 ks + 8 hh + j]
+  u32x4 kf[KS], vf[KS];
+  {
+    const bool kval = kj < Lk;
+    const uint16_t* krow = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2] + (int64_t)(kval ? kj : 0) * p.k_stride[1];
+    const uint16_t* vrow = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2] + (int64_t)(kval ? kj : 0) * p.v_stride[1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = load_row_frag<ALIGNED>(krow, 16 * ks + 8 * hh, D, kval);
+      vf[ks] = load_row_frag<ALIGNED>(vrow, 16 * ks + 8 * hh, D, kval);
+    }
+  }
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  // query tiles: causal -> the first row that sees key n0 is n0 - diag
+  int m_begin = 0;
+  if (CAUSAL) m_begin = max(0, n0 - diag) & ~(BMQ - 1);
+  const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
+  const int total = n_mt * G;  // (q-head, tile) steps
+
+  auto qt = [&](int buf) { return smem + buf * 2 * TILE; };
+  auto ot = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
+  auto stage = [&](int step, int buf) {
+    const int g = step / n_mt, mt = step - g * n_mt;
+    const int hq = hkv * G + g;
+    const int m = m_begin + mt * BMQ;
+    const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
+    const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
+    stage_tile<DT, BMQ, NT, ALIGNED>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
+    stage_tile<DT, BMQ, NT, ALIGNED>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
+  };
+  if (total > 0) stage(0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  for (int step = 0; step < total; ++step) {
+    const int cur = step & 1;
+    if (step + 1 < total) stage(step + 1, cur ^ 1);
+    const int g = step / n_mt, mt = step - g * n_mt;
+    const int hq = hkv * G + g;
+    const int m = m_begin + mt * BMQ;
+    const char* Q = qt(cur);
+    const char* O = ot(cur);
+
+    // does any (query, key) of this wave survive the masks?
+    const bool active = kw0 < Lk && (!CAUSAL || kw0 <= m + BMQ - 1 + diag);
+    if (active) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT>(Q, r32, 2 * ks + hh), kf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT>(O, r32, 2 * ks + hh), vf[ks], dp);
+
+      // row statistics of the 16 query rows held in registers: rows m + 8 g4 + 4 hh + (0..3)
+      const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m;
+      f32x4 lse4[4], del4[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        lse4[g4] = *(const f32x4*)(p.lse + srow + 8 * g4 + 4 * hh);
+        del4[g4] = *(const f32x4*)(p.delta + srow + 8 * g4 + 4 * hh);
+      }
+      const bool need_mask = (kw0 + 31 >= Lk) || (m + BMQ > Lq) || (CAUSAL && kw0 + 31 > m + diag);
+      u32x4 pp[2], dsp[2];
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        float pv[8], dsv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * sp + j;
+          const int qrow = m + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          float x = s[i] * scale2;
+          if (BIAS) {
+            const int qc = qrow < Lq ? qrow : Lq - 1;
+            const int kc = kj < Lk ? kj : Lk - 1;
+            x += kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                                (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
+          }
+          float pr = __builtin_amdgcn_exp2f(x - lse4[i >> 2 & 3][i & 3]);
+          if (need_mask) {
+            bool ok = kj < Lk && qrow < Lq;
+            if (CAUSAL) ok = ok && (kj <= qrow + diag);
+            pr = ok ? pr : 0.f;
+          }
+          pv[j] = pr;
+          dsv[j] = pr * (dp[i] - del4[i >> 2 & 3][i & 3]) * scale;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pp[sp][j] = E::pack2(pv[2 * j], pv[2 * j + 1]);
+          dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          dv[dt] = E::mfma(lds_tr_frag<DT>(O, 16 * sp, 32 * dt, lane), pp[sp], dv[dt]);
+          dk[dt] = E::mfma(lds_tr_frag<DT>(Q, 16 * sp, 32 * dt, lane), dsp[sp], dk[dt]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  // ---- store dK, dV (kv heads; fp32 group sum rounded once) ----------------------------
+  if (kj < p.seqlen_k) {
+    const bool kval = kj < Lk;
+    uint16_t* dkrow = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kj * p.dk_stride[1];
+    uint16_t* dvrow = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kj * p.dv_stride[1];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        float a[4], c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = kval ? dk[dt][4 * g4 + j] : 0.f;
+          c[j] = kval ? dv[dt][4 * g4 + j] : 0.f;
+        }
+        if (ALIGNED) {
+          if (d0 < D) {
+            *(u32x2*)(dkrow + d0) = u32x2{E::pack2(a[0], a[1]), E::pack2(a[2], a[3])};
+            *(u32x2*)(dvrow + d0) = u32x2{E::pack2(c[0], c[1]), E::pack2(c[2], c[3])};
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (d0 + j < D) {
+              dkrow[d0 + j] = E::from_f32(a[j]);
+              dvrow[d0 + j] = E::from_f32(c[j]);
+            }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dQ: one workgroup = 4 waves = 128 query rows of one (batch, q-head); K/V tiles of 64 keys in
+// LDS (double buffered).  Per tile and wave:
+//   S^T, dP^T [key][q]   2 x (8 + 8) MFMA (A = K / V row fragments, B = Q / dO in VGPRs)
+//   dQ^T[d][q] += K^T dS^T   NDT*4 MFMA (A = K^T via ds_read_b64_tr_b16)
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED, bool DQF32>
+__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int NT = 256;
+  constexpr int BM = 128, BN = 64;
+  constexpr int KS = DT / 16;
+  constexpr int NDT = DT / 32;
+  constexpr int TILE = BN * DT * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nmb = gridDim.x;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
+  const int hkv = hq / (p.heads_q / p.heads_kv);
+  int Lq = p.seqlen_q, Lk = p.seqlen_k;
+  if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+  const int D = p.head_dim;
+  const int diag = Lk - Lq;
+  const int m0 = mb * BM;
+  const int mw0 = m0 + 32 * w;
+  const int qi = mw0 + r32;
+  const float scale = p.softmax_scale, scale2 = scale * kLog2e;
+
+  const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
+  const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
+  int n_end = 0;
+  if (m0 < Lq) {
+    n_end = Lk;
+    if (CAUSAL) n_end = min(Lk, m0 + BM + diag);
+    n_end = max(n_end, 0);
+  }
+  const int ntiles = (n_end + BN - 1) / BN;
+  auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
+  auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
+  if (ntiles > 0) {
+    stage_tile<DT, BN, NT, ALIGNED>(kt(0), kg, p.k_stride[1], 0, Lk, D, tid);
+    stage_tile<DT, BN, NT, ALIGNED>(vt(0), vg, p.v_stride[1], 0, Lk, D, tid);
+  }
+
+  const bool qvalid = qi < Lq;
+  u32x4 qf[KS], of[KS];
+  {
+    const uint16_t* qrow = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2] + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
+    const uint16_t* orow = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2] + (int64_t)(qvalid ? qi : 0) * p.do_stride[1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qf[ks] = load_row_frag<ALIGNED>(qrow, 16 * ks + 8 * hh, D, qvalid);
+      of[ks] = load_row_frag<ALIGNED>(orow, 16 * ks + 8 * hh, D, qvalid);
+    }
+  }
+  const int64_t srow = (int64_t)bh * p.lse_row_stride;
+  const float lse_i = qvalid ? p.lse[srow + qi] : 0.f;
+  const float del_i = qvalid ? p.delta[srow + qi] : 0.f;
+
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
+
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const int n0 = it * BN;
+    if (it + 1 < ntiles) {
+      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
+      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
+    }
+    const char* K = kt(cur);
+    const char* V = vt(cur);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kt0 = n0 + 32 * t;
+      const bool active = kt0 < Lk && (!CAUSAL || kt0 <= mw0 + 31 + diag);
+      if (!active) continue;
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT>(K, 32 * t + r32, 2 * ks + hh), qf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT>(V, 32 * t + r32, 2 * ks + hh), of[ks], dp);
+      const bool need_mask = (kt0 + 31 >= Lk) || !qvalid || (CAUSAL && kt0 + 31 > mw0 + diag) || (mw0 + 31 >= Lq);
+      u32x4 dsp[2];
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        float dsv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * sp + j;
+          const int kj = kt0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          float x = s[i] * scale2;
+          if (BIAS) {
+            const int kc = kj < Lk ? kj : Lk - 1;
+            const int qc = qvalid ? qi : 0;
+            x += kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                                (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
+          }
+          float pr = __builtin_amdgcn_exp2f(x - lse_i);
+          if (need_mask) {
+            bool ok = kj < Lk && qvalid;
+            if (CAUSAL) ok = ok && (kj <= qi + diag);
+            pr = ok ? pr : 0.f;
+          }
+          dsv[j] = pr * (dp[i] - del_i) * scale;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+          acc[dt] = E::mfma(lds_tr_frag<DT>(K, 32 * t + 16 * sp, 32 * dt, lane), dsp[sp], acc[dt]);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  if (qi < p.seqlen_q) {
+    const bool ok = qvalid;
+    char* base = (char*)p.dq;
+    const int esz = DQF32 ? 4 : 2;
+    char* row = base + (int64_t)esz * (b * p.dq_stride[0] + hq * p.dq_stride[2] + (int64_t)qi * p.dq_stride[1]);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        float a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = ok ? acc[dt][4 * g4 + j] : 0.f;
+        if (DQF32) {
+          float* r = (float*)row;
+          if (ALIGNED) {
+            if (d0 < D) *(f32x4*)(r + d0) = f32x4{a[0], a[1], a[2], a[3]};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (d0 + j < D) r[d0 + j] = a[j];
+          }
+        } else {
+          uint16_t* r = (uint16_t*)row;
+          if (ALIGNED) {
+            if (d0 < D) *(u32x2*)(r + d0) = u32x2{E::pack2(a[0], a[1]), E::pack2(a[2], a[3])};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) if (d0 + j < D) r[d0 + j] = E::from_f32(a[j]);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
+static hipError_t launch_bwd_t(const fa2_bwd_args& a, hipStream_t st) {
+  {
+    dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
+    hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
+  }
+  {
+    dim3 grid((a.seqlen_k + 127) / 128, a.batch * a.heads_kv);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED>), grid, dim3(256), 0, st, a);
+  }
+  {
+    dim3 grid((a.seqlen_q + 127) / 128, a.batch * a.heads_q);
+    if (a.dq_dtype == FA2_F32)
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, false>), grid, dim3(256), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+template <bool BF16, int DT>
+hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, hipStream_t st) {
+  const bool c = a.causal != 0, bi = a.bias != nullptr;
+#define FA2_BWD_CASE(C, B, A) \
+  if (c == C && bi == B && aligned == A) return launch_bwd_t<BF16, DT, C, B, A>(a, st);
+  FA2_BWD_CASE(true, true, true)
+  FA2_BWD_CASE(true, true, false)
+  FA2_BWD_CASE(true, false, true)
+  FA2_BWD_CASE(true, false, false)
+  FA2_BWD_CASE(false, true, true)
+  FA2_BWD_CASE(false, true, false)
+  FA2_BWD_CASE(false, false, true)
+  FA2_BWD_CASE(false, false, false)
+#undef FA2_BWD_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace fa2

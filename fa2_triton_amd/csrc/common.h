@@ -1,0 +1,239 @@
+// common.h -- CDNA4 (gfx950) building blocks shared by the forward and backward kernels.
+//
+// * MFMA: v_mfma_f32_32x32x16_{bf16,f16}.  Lane l (r = l & 31, h = l >> 5) holds
+//     A[row r][k = 8h + j], B[k = 8h + j][col r]  (j = 0..7, one 16-byte fragment each),
+//     C[row (i & 3) + 8 (i >> 2) + 4h][col r]    (i = 0..15, f32).
+//   Every product in these kernels is arranged "swapped" (S^T = K Q^T, O^T = V^T P^T, ...)
+//   so that the softmax row (one query) sits on one lane pair (l, l ^ 32): row statistics
+//   are per-lane scalars and the probability accumulator is already the B operand of the next
+//   product (the k order inside a 16-wide k-step is then 8(j>>2) + 4h + (j&3); the other
+//   operand is read in that same order through ds_read_b64_tr_b16).
+// * LDS tiles are [rows][DT] 16-bit elements with 16-byte chunks XOR-swizzled per row so that
+//   both 16-byte row reads (ds_read_b128, A/B fragments) and 4-row transposed reads
+//   (ds_read_b64_tr_b16) are bank-conflict free (swizzle below).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fa2 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+#define FA2_DEV __device__ __forceinline__
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kNegInf = -__builtin_inff();
+
+// ---------------------------------------------------------------------------------------------
+// Element traits: raw 16-bit storage, conversions and the matching MFMA.
+template <bool BF16>
+struct Elem;
+
+template <>
+struct Elem<true> {
+  FA2_DEV static float to_f32(uint16_t x) { return __uint_as_float(uint32_t(x) << 16); }
+  FA2_DEV static uint16_t from_f32(float x) {
+    __bf16 b = (__bf16)x;  // RNE, v_cvt_pk_bf16_f32 on gfx950
+    return __builtin_bit_cast(uint16_t, b);
+  }
+  FA2_DEV static uint32_t pack2(float lo, float hi) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  FA2_DEV static f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
+template <>
+struct Elem<false> {
+  FA2_DEV static float to_f32(uint16_t x) { return (float)__builtin_bit_cast(_Float16, x); }
+  FA2_DEV static uint16_t from_f32(float x) {
+    _Float16 h = (_Float16)x;
+    return __builtin_bit_cast(uint16_t, h);
+  }
+  FA2_DEV static uint32_t pack2(float lo, float hi) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    f16x2 v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  FA2_DEV static f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+// Bias element loads (bias may be f16, bf16 or f32; code 16 / 17 / 32 as encode_dtype).
+FA2_DEV float load_bias(const void* base, int64_t idx, int code) {
+  if (code == 32) return ((const float*)base)[idx];
+  uint16_t x = ((const uint16_t*)base)[idx];
+  return code == 17 ? Elem<true>::to_f32(x) : Elem<false>::to_f32(x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross-half exchange: returns {x of lanes 0-31, x of lanes 32-63} in every lane.
+FA2_DEV float half_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+FA2_DEV float half_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+FA2_DEV f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS tile layout.  A tile is `rows` x DT 16-bit elements (DT in {32, 64, 128, 256}), row
+// pitch 2*DT bytes, 16-byte chunk c of row r stored at chunk c ^ swz(r).  The swizzle keeps
+//  (a) a ds_read_b128 lane group (16 lanes, 16 distinct rows, one chunk each) on 16 distinct
+//      16-byte slots of the 256-byte bank row, and
+//  (b) a ds_read_b64_tr_b16 half wave (4 consecutive rows x 4 consecutive chunks) on 16
+//      distinct slots as well.
+template <int DT>
+struct Tile {
+  static constexpr int kRowBytes = DT * 2;
+  static constexpr int kChunks = DT / 8;
+  FA2_DEV static int swz(int r) {
+    if constexpr (DT == 32) return (r >> 2) & 3;
+    else if constexpr (DT == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+    else return ((r & 3) << 2) | ((r >> 2) & 3);
+  }
+  // byte offset of chunk c of row r
+  FA2_DEV static int off(int r, int c) { return r * kRowBytes + ((c ^ swz(r)) << 4); }
+};
+
+// 16-byte row fragment: row r, chunk c  (A or B operand of a 32x32x16 MFMA).
+template <int DT>
+FA2_DEV u32x4 lds_row_frag(const char* tile, int r, int c) {
+  return *(const u32x4*)(tile + Tile<DT>::off(r, c));
+}
+
+// Transposed fragment for the operand whose k index runs over tile ROWS:
+// element j of lane (r32 = l & 31, h = l >> 5) = tile[row0 + 8 (j >> 2) + 4 h + (j & 3)][col0 + r32]
+// (the permuted k order matching a C-layout accumulator reused as the other operand).
+template <int DT>
+FA2_DEV u32x4 lds_tr_frag(const char* tile, int row0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * (i & 3);
+  const int c = col >> 3, half = (col >> 2) & 1;
+  const int ra = row0 + 4 * h + (i >> 2);
+  const int rb = ra + 8;
+  const lds_char* pa = (const lds_char*)(tile + Tile<DT>::off(ra, c) + half * 8);
+  const lds_char* pb = (const lds_char*)(tile + Tile<DT>::off(rb, c) + half * 8);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
+  u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  return u32x4{a[0], a[1], b[0], b[1]};
+}
+
+// ---------------------------------------------------------------------------------------------
+// Global -> LDS tile staging.  `rows` rows starting at global row `row0` (row stride
+// `row_stride` elements) of a [*, D] slice; rows >= row_end and columns >= D must not leak
+// NaN/Inf garbage into the MFMAs, so:
+//  ALIGNED (D % 8 == 0, 16-byte aligned rows): LDS-DMA 16-byte pieces
+//    (global_load_lds_dwordx4: LDS destination = wave base + lane*16, so the swizzle is applied
+//    to the per-lane SOURCE address); out-of-range rows / chunks are clamped to valid memory
+//    (finite data that is masked out of every result).
+//  otherwise: element loads with zero fill + ds_write.
+template <int DT, int ROWS, int NTHREADS, bool ALIGNED>
+FA2_DEV void stage_tile(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end,
+                        int D, int tid) {
+  constexpr int kChunks = DT / 8;
+  constexpr int kPieces = ROWS * kChunks;  // 16-byte pieces in the tile
+  if constexpr (ALIGNED) {
+    static_assert(kPieces % 64 == 0, "tile must be a whole number of wave pieces");
+    const int wave = tid >> 6, lane = tid & 63;
+    const int dchunks = D >> 3;
+#pragma unroll
+    for (int it = 0; it < (kPieces + NTHREADS - 1) / NTHREADS; ++it) {
+      const int wbase = (it * (NTHREADS / 64) + wave) * 64;  // first piece of this wave
+      if (kPieces % NTHREADS != 0 && wbase >= kPieces) break;  // wave-uniform
+      const int piece = wbase + lane;
+      const int pr = piece / kChunks;            // physical row
+      const int pc = piece % kChunks;            // physical chunk
+      const int c = pc ^ Tile<DT>::swz(pr);      // logical chunk stored there
+      int grow = row0 + pr;
+      grow = grow < row_end ? grow : row_end - 1;
+      const int gc = c < dchunks ? c : dchunks - 1;
+      const uint16_t* src = g + (int64_t)grow * row_stride + gc * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(tile + wbase * 16),
+                                       16, 0, 0);
+    }
+  } else {
+    // one thread per (row, chunk); 8 scalar loads each
+    for (int piece = tid; piece < kPieces; piece += NTHREADS) {
+      const int r = piece / kChunks, c = piece % kChunks;
+      const int grow = row0 + r;
+      uint16_t vals[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = c * 8 + j;
+        vals[j] = (grow < row_end && d < D) ? g[(int64_t)grow * row_stride + d] : (uint16_t)0;
+      }
+      u32x4 pk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pk[j] = uint32_t(vals[2 * j]) | (uint32_t(vals[2 * j + 1]) << 16);
+      *(u32x4*)(tile + Tile<DT>::off(r, c)) = pk;
+    }
+  }
+}
+
+// 16-byte register fragment straight from global memory: elements [d0, d0 + 8) of one row;
+// zero outside [0, D) or when !valid.
+template <bool ALIGNED>
+FA2_DEV u32x4 load_row_frag(const uint16_t* row, int d0, int D, bool valid) {
+  if constexpr (ALIGNED) {
+    if (valid && d0 < D) return *(const u32x4*)(row + d0);
+    return u32x4{0u, 0u, 0u, 0u};
+  } else {
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (valid && d0 + j < D) ? row[d0 + j] : (uint16_t)0;
+    u32x4 pk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pk[j] = uint32_t(v[2 * j]) | (uint32_t(v[2 * j + 1]) << 16);
+    return pk;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10, first output word, counter (lo, hi, 0, 0), key (seed_lo, seed_hi), converted
+// to [0,1) exactly like Triton's tl.rand (triton/language/random.py:13-156; see
+// oracle/philox.py).  Used for the forward dropout mask keep = rand > p
+// (/root/reference/src/forward/compute_row_blocks.py:76-79).
+FA2_DEV float philox_uniform(uint64_t seed, uint64_t offset) {
+  uint32_t c0 = (uint32_t)offset, c1 = (uint32_t)(offset >> 32), c2 = 0, c3 = 0;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t a0 = c0, a2 = c2;
+    c0 = __umulhi(0xCD9E8D57u, a2) ^ c1 ^ k0;
+    c2 = __umulhi(0xD2511F53u, a0) ^ c3 ^ k1;
+    c1 = 0xCD9E8D57u * a2;
+    c3 = 0xD2511F53u * a0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  int32_t x = (int32_t)c0;
+  x = x < 0 ? -x - 1 : x;
+  return (float)x * 4.6566127342e-10f;
+}
+
+}  // namespace fa2

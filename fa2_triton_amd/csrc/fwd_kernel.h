@@ -1,0 +1,250 @@
+// fwd.hip -- FlashAttention-2 forward for gfx950 (CDNA4).
+//
+// Replaces _fwd_kernel + compute_row_block (/root/reference/src/forward/kernel.py:61-291,
+// /root/reference/src/forward/compute_row_blocks.py:7-103) with the same semantics:
+//   s_ij = scale * <q_i, k_j> + bias_ij, bottom-right causal (j <= i + Lk - Lq), key padding,
+//   online softmax in base 2, optional Philox dropout on P after the row sum, O = P V / l,
+//   LSE2_i = m_i + log2(l_i) (kernel.py:119, compute_row_blocks.py:58-101).
+//
+// Work decomposition: one workgroup = NW waves = NW*32 query rows of one (batch, q-head);
+// each wave owns 32 rows.  K/V tiles of 64 keys are staged in LDS (double buffered, LDS-DMA)
+// and shared by the waves.  Per 64-key tile and wave:
+//   S^T[key][q] = K Q^T        16 MFMA 32x32x16 (A = K row frags from LDS, B = Q frags in VGPRs)
+//   softmax on the lane pair (l, l^32) holding one query row (16+16 keys per 32-key tile)
+//   O^T[d][q]  += V^T P^T      16 MFMA (A = V^T via ds_read_b64_tr_b16, B = P in registers)
+#include "common.h"
+#include "fa2_internal.h"
+
+namespace fa2 {
+
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
+__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_fwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int NW = 4;
+  constexpr int NT = NW * 64;
+  constexpr int BM = NW * 32;        // query rows per workgroup
+  constexpr int BN = 64;             // keys per tile
+  constexpr int KS = DT / 16;        // k-steps of Q K^T
+  constexpr int NDT = DT / 32;       // 32-wide d tiles of O
+  constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 V0 K1 V1
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+
+  // ---- work item -----------------------------------------------------------------------
+  const int nmb = gridDim.x;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heavy rows first
+  const int bh = blockIdx.y;
+  const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
+  const int hkv = hq / (p.heads_q / p.heads_kv);
+  int Lq = p.seqlen_q, Lk = p.seqlen_k, cu = 0;
+  if (p.cu_seqlens) {
+    cu = p.cu_seqlens[b];
+    Lq = Lk = p.cu_seqlens[b + 1] - cu;
+  }
+  const int m0 = mb * BM;
+  const int qi = m0 + w * 32 + r32;  // this lane's query row
+  const int D = p.head_dim;
+
+  const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
+  const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
+  const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
+
+  // key range of the workgroup
+  int n_end = 0;
+  if (m0 < Lq) {
+    n_end = Lk;
+    if (CAUSAL) n_end = min(Lk, m0 + BM + Lk - Lq);
+    n_end = max(n_end, 0);
+  }
+  const int ntiles = (n_end + BN - 1) / BN;
+
+  // stage tile 0 first so its latency overlaps the Q fragment loads
+  auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
+  auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
+  if (ntiles > 0) {
+    stage_tile<DT, BN, NT, ALIGNED>(kt(0), kg, p.k_stride[1], 0, Lk, D, tid);
+    stage_tile<DT, BN, NT, ALIGNED>(vt(0), vg, p.v_stride[1], 0, Lk, D, tid);
+  }
+
+  // ---- Q fragments (B operand of S^T = K Q^T): Q[qi][16 ks + 8 hh + j] -------------------
+  u32x4 qf[KS];
+  {
+    const bool qvalid = qi < Lq;
+    const uint16_t* qrow = qg + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = load_row_frag<ALIGNED>(qrow, 16 * ks + 8 * hh, D, qvalid);
+  }
+
+  const float scale2 = p.softmax_scale * kLog2e;
+  const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
+  float m_run = kNegInf, l_run = 0.f;
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
+
+  const char* biasb = nullptr;
+  if (BIAS)
+    biasb = (const char*)p.bias;
+  uint64_t drop_base = 0;
+  if (DROPOUT) {
+    // flat Philox offset, /root/reference/src/forward/kernel.py:146-148 (int64 here)
+    drop_base = (uint64_t)Lk * ((uint64_t)cu + (uint64_t)Lq * ((uint64_t)hq + (uint64_t)p.heads_q * (p.cu_seqlens ? 0 : b)));
+  }
+
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const int n0 = it * BN;
+    if (it + 1 < ntiles) {  // prefetch the next K/V tile into the other buffer
+      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
+      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
+    }
+    const char* K = kt(cur);
+    const char* V = vt(cur);
+
+    // ---- S^T = K Q^T for two 32-key halves --------------------------------------------
+    f32x16 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      s[t] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s[t] = E::mfma(lds_row_frag<DT>(K, 32 * t + r32, 2 * ks + hh), qf[ks], s[t]);
+    }
+
+    // ---- scores in base 2, masks --------------------------------------------------------
+    // key of register i in half t: n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
+    const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > m0 + w * 32 + diag));
+    float mx = kNegInf;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        float x = s[t][i] * scale2;
+        if (BIAS) {
+          const int kc = kj < Lk ? kj : Lk - 1;
+          const int qc = qi < Lq ? qi : 0;
+          x += kLog2e * load_bias(biasb, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                             (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
+        }
+        if (need_mask) {
+          bool ok = kj < Lk;
+          if (CAUSAL) ok = ok && (kj <= qi + diag);
+          x = ok ? x : kNegInf;
+        }
+        s[t][i] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+    mx = half_max(mx);
+    const float m_new = fmaxf(m_run, mx);
+    const float m_use = m_new == kNegInf ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+
+    float rs = 0.f;
+    u32x4 pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float pv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        pv[i] = exp2f(s[t][i] - m_use);
+        rs += pv[i];
+      }
+      if (DROPOUT) {
+        const uint64_t rowoff = drop_base + (uint64_t)qi * Lk;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const float u = philox_uniform(p.dropout_seed, rowoff + kj);
+          pv[i] = u > p.dropout_p ? pv[i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pf[t][sp][j] = E::pack2(pv[8 * sp + 2 * j], pv[8 * sp + 2 * j + 1]);
+    }
+    l_run = l_run * alpha + rs;  // lane-partial row sum (the partner lane holds the rest)
+
+    // ---- O^T = alpha O^T + V^T P^T ---------------------------------------------------------
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+          acc[dt] = E::mfma(lds_tr_frag<DT>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
+    }
+
+    __builtin_amdgcn_s_waitcnt(0);  // next tile landed (LDS-DMA counts on vmcnt)
+    __syncthreads();
+  }
+
+  // ---- epilogue ----------------------------------------------------------------------------
+  const float l_tot = half_sum(l_run);
+  const bool row_ok = qi < Lq && l_tot > 0.f;
+  float inv = row_ok ? 1.f / l_tot : 0.f;
+  if (DROPOUT) inv *= 1.f / (1.f - p.dropout_p);
+  if (hh == 0 && qi < p.lse_row_stride) {
+    float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
+    lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
+  }
+  if (qi < p.seqlen_q) {
+    uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        const float o0 = acc[dt][4 * g4 + 0] * inv, o1 = acc[dt][4 * g4 + 1] * inv;
+        const float o2 = acc[dt][4 * g4 + 2] * inv, o3 = acc[dt][4 * g4 + 3] * inv;
+        if (ALIGNED) {
+          if (d0 < D) *(u32x2*)(orow + d0) = u32x2{E::pack2(o0, o1), E::pack2(o2, o3)};
+        } else {
+          if (d0 + 0 < D) orow[d0 + 0] = E::from_f32(o0);
+          if (d0 + 1 < D) orow[d0 + 1] = E::from_f32(o1);
+          if (d0 + 2 < D) orow[d0 + 2] = E::from_f32(o2);
+          if (d0 + 3 < D) orow[d0 + 3] = E::from_f32(o3);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
+static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
+  constexpr int BM = 128;
+  dim3 grid((a.seqlen_q + BM - 1) / BM, a.batch * a.heads_q);
+  hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <bool BF16, int DT>
+hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
+  const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
+#define FA2_FWD_CASE(C, B, R, A)                                  \
+  if (c == C && bi == B && dr == R && aligned == A)               \
+    return launch_fwd_t<BF16, DT, C, B, R, A>(a, st);
+#define FA2_FWD_A(C, B, R) FA2_FWD_CASE(C, B, R, true) FA2_FWD_CASE(C, B, R, false)
+#define FA2_FWD_R(C, B) FA2_FWD_A(C, B, true) FA2_FWD_A(C, B, false)
+#define FA2_FWD_B(C) FA2_FWD_R(C, true) FA2_FWD_R(C, false)
+  FA2_FWD_B(true)
+  FA2_FWD_B(false)
+#undef FA2_FWD_B
+#undef FA2_FWD_R
+#undef FA2_FWD_A
+#undef FA2_FWD_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace fa2

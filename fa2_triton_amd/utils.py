@@ -1,0 +1,89 @@
+"""Host helpers of the reference (/root/reference/src/utils.py) that survive the move to HIP.
+
+The device helper `load_fn` (:34-54) folds into the kernels' tile loads; the host varlen
+pack/unpack loops (:8-31) are replaced by in-place padded-tensor handling in the kernels plus
+`cu_seqlens_from_mask` (device-side, no .item() synchronisation).
+"""
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+
+def infer_bias_strides(
+    bias: Optional[Tensor], batch: int, nheads_q: int, seqlen_q: int, seqlen_k: int
+) -> Tuple[int, int, int]:
+    """Broadcast strides (batch, head, row) of an additive bias [1|B, 1|Hq, Sq, Sk].
+
+    Same contract as /root/reference/src/utils.py:57-77, except that a per-head bias
+    [., Hq, ., .] is accepted (the reference compares stride(1) with nheads_q at :70, which
+    rejects it) and is indexed by the query head in forward and backward alike (the reference
+    uses the kv head in forward, src/forward/kernel.py:141, and the q head in backward,
+    src/backward/kernel.py:143).
+    """
+    if bias is None:
+        return 0, 0, 0
+    assert bias.dim() == 4 and bias.size(2) == seqlen_q and bias.size(3) == seqlen_k, f"{bias.shape = }"
+    if bias.size(0) == 1:
+        stride_bb = 0
+    elif bias.size(0) == batch:
+        stride_bb = bias.stride(0)
+    else:
+        raise ValueError(f"Attention bias has {bias.size(0) = } while {batch = }")
+    if bias.size(1) == 1:
+        stride_bh = 0
+    elif bias.size(1) == nheads_q:
+        stride_bh = bias.stride(1)
+    else:
+        raise ValueError(f"Attention bias has {bias.size(1) = } while {nheads_q = }")
+    if bias.stride(3) != 1:
+        raise ValueError("Attention bias must have a contiguous last dimension")
+    return stride_bb, stride_bh, bias.stride(2)
+
+
+def handle_dropout(dropout_p: float, dropout_seed: Optional[int], is_forward: bool) -> int:
+    """Seed handling of /root/reference/src/utils.py:80-88 (backward dropout unsupported)."""
+    assert dropout_p >= 0, f"Dropout probability {dropout_p = } must be above 0."
+    assert dropout_p < 1, f"Dropout probability {dropout_p = } must be strictly below 1."
+    if dropout_p == 0:
+        return 0
+    if is_forward:
+        return torch.randint(low=0, high=2**32, size=(1,)).item() if dropout_seed is None else dropout_seed
+    raise NotImplementedError("Backward pass does not yet support dropout.")
+
+
+def encode_dtype(x: Tensor) -> int:
+    """dtype code, /root/reference/src/utils.py:102-109 (also the C ABI's fa2_dtype)."""
+    if x.dtype == torch.float16:
+        return _lib.FA2_F16
+    if x.dtype == torch.bfloat16:
+        return _lib.FA2_BF16
+    if x.dtype == torch.float32:
+        return _lib.FA2_F32
+    raise ValueError(x.dtype)
+
+
+def bshd_strides(x: Tensor) -> Tuple[int, int, int]:
+    """(batch, seq, head) element strides of a [B, S, H, D] view with unit last stride."""
+    assert x.stride(-1) == 1, "last dimension must be contiguous"
+    return x.stride(0), x.stride(1), x.stride(2)
+
+
+def stream_of(x: Tensor) -> int:
+    return torch.cuda.current_stream(x.device).cuda_stream
+
+
+def cu_seqlens_from_mask(attention_mask: Tensor) -> Tensor:
+    """[B+1] int32 cumulative valid lengths of a right-padded [B, S] mask, computed on device."""
+    mask = attention_mask
+    if mask.dtype != torch.bool:
+        mask = mask != 0
+    mask = mask.contiguous()
+    batch, seqlen = mask.shape
+    cu = torch.empty(batch + 1, dtype=torch.int32, device=mask.device)
+    lib = _lib.load()
+    _lib.check(lib.fa2_cu_seqlens_from_mask(mask.data_ptr(), mask.stride(0), batch, seqlen, cu.data_ptr(),
+                                            stream_of(mask)))
+    return cu

@@ -1,0 +1,83 @@
+"""Public autograd op -- same surface as /root/reference/src/wrapper.py:10-100.
+
+`flash_attn_func(q, k, v, attention_mask=None, attention_bias=None, dropout_p=0.0,
+causal=False, softmax_scale=None, dropout_seed=None)` with q [B, Sq, Hq, D], k/v
+[B, Sk, Hkv, D] (fp16 / bf16), returns O [B, Sq, Hq, D].  Backward returns (dq, dk, dv) and
+no gradient for the mask, bias and scalars, exactly as the reference (:62-86).
+"""
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from .backward import _flash_attn_backward
+from .forward import _flash_attn_forward
+
+
+class FlashAttnFunc(torch.autograd.Function):
+    @staticmethod
+    def forward(
+        ctx,
+        q: Tensor,
+        k: Tensor,
+        v: Tensor,
+        attention_mask: Optional[Tensor] = None,
+        attention_bias: Optional[Tensor] = None,
+        dropout_p: float = 0.0,
+        causal: bool = False,
+        softmax_scale: Optional[float] = None,
+        dropout_seed: Optional[int] = None,
+    ):
+        # only the last dimension has to be contiguous (reference :41-43); bias fully (:44)
+        q = q if q.stride(-1) == 1 else q.contiguous()
+        k = k if k.stride(-1) == 1 else k.contiguous()
+        v = v if v.stride(-1) == 1 else v.contiguous()
+        attention_bias = None if attention_bias is None else attention_bias.contiguous()
+        o, lse, ctx.softmax_scale, ctx.dropout_seed = _flash_attn_forward(
+            q=q,
+            k=k,
+            v=v,
+            attention_mask=attention_mask,
+            bias=attention_bias,
+            dropout_p=dropout_p,
+            causal=causal,
+            softmax_scale=softmax_scale,
+            dropout_seed=dropout_seed,
+        )
+        ctx.save_for_backward(q, k, v, attention_bias, attention_mask, o, lse)
+        ctx.causal = causal
+        ctx.dropout_p = dropout_p
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, bias, attention_mask, o, lse = ctx.saved_tensors
+        dq, dk, dv = _flash_attn_backward(
+            dO=do,
+            q=q,
+            k=k,
+            v=v,
+            bias=bias,
+            attention_mask=attention_mask,
+            o=o,
+            lse=lse,
+            dropout_p=ctx.dropout_p,
+            causal=ctx.causal,
+            softmax_scale=ctx.softmax_scale,
+            dropout_seed=ctx.dropout_seed,
+        )
+        return dq, dk, dv, None, None, None, None, None, None
+
+
+def flash_attn_func(
+    q: Tensor,
+    k: Tensor,
+    v: Tensor,
+    attention_mask: Optional[Tensor] = None,
+    attention_bias: Optional[Tensor] = None,
+    dropout_p: float = 0.0,
+    causal: bool = False,
+    softmax_scale: Optional[float] = None,
+    dropout_seed: Optional[int] = None,
+) -> Tensor:
+    return FlashAttnFunc.apply(q, k, v, attention_mask, attention_bias, dropout_p, causal, softmax_scale, dropout_seed)

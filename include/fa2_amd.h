@@ -1,0 +1,124 @@
+/*
+ * fa2_amd.h -- C ABI of the MI355X (gfx950) FlashAttention-2 forward/backward kernels.
+ *
+ * This library replaces the three Triton launches of the reference
+ * (remi-or/fa2_triton @ 2024-10-08):
+ *   fa2_fwd  <- _fwd_kernel[grid](...)      /root/reference/src/forward/caller.py:83-116
+ *   fa2_bwd  <- _compute_delta[grid](...)   /root/reference/src/backward/caller.py:95-114
+ *             + _bwd_kernel[grid](...)      /root/reference/src/backward/caller.py:122-160
+ *             + the host GQA dK/dV sum      /root/reference/src/backward/caller.py:162-165
+ * and the host varlen pack/unpack loops (/root/reference/src/utils.py:8-31) through
+ *   fa2_cu_seqlens_from_mask  (device-side cumulative lengths of a right-padded mask).
+ *
+ * Conventions
+ *  - All tensors live in device memory and are addressed by element strides; the last
+ *    (head_dim) stride must be 1 (/root/reference/src/wrapper.py:41-43).  Q/K/V/O/dO/dQ/dK/dV
+ *    use the reference's [batch, seqlen, heads, head_dim] (BSHD) indexing, but any stride
+ *    order works (e.g. BHSD views), so no copies are needed.
+ *  - lse / delta are [batch, heads_q, lse_row_stride] fp32, lse_row_stride >= seqlen_q
+ *    (the reference rounds it up to a multiple of 128, src/forward/caller.py:73-74).
+ *    lse holds the base-2 log-sum-exp: LSE2 = ln(sum_j exp(s_ij)) * log2(e); rows with no
+ *    visible key (causal seqlen_q > seqlen_k, padded rows) hold -inf.
+ *  - Nothing is allocated inside the library; every buffer is caller-owned.
+ *  - Launches are asynchronous on `stream` (a hipStream_t; NULL = default stream).
+ *  - Return 0 on success or a negative FA2_E* code; fa2_last_error() then describes it
+ *    (thread-local string).  The Python host layer raises RuntimeError with that text.
+ */
+#ifndef FA2_AMD_H
+#define FA2_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA2_ABI_VERSION 1
+
+/* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
+enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
+
+enum fa2_status {
+  FA2_OK = 0,
+  FA2_E_INVALID = -1,     /* bad shape / stride / pointer */
+  FA2_E_UNSUPPORTED = -2, /* valid but not implemented (e.g. head_dim > 256) */
+  FA2_E_HIP = -3          /* a HIP runtime call failed */
+};
+
+/* Forward: O = softmax(scale * Q K^T + bias, masks) V  (dropout optional), plus LSE2.
+ * Mirrors the argument list of _fwd_kernel (/root/reference/src/forward/kernel.py:61-96). */
+typedef struct fa2_fwd_args {
+  const void* q;      /* [B, Sq, Hq, D] */
+  const void* k;      /* [B, Sk, Hkv, D] */
+  const void* v;      /* [B, Sk, Hkv, D] */
+  void* o;            /* [B, Sq, Hq, D], same dtype as q; every element is written */
+  float* lse;         /* [B, Hq, lse_row_stride]; rows [0, Sq) written */
+  const void* bias;   /* optional additive bias [1|B, 1|Hq, Sq, Sk] (strides below), or NULL */
+  const int32_t* cu_seqlens; /* optional [B+1] cumulative valid lengths (varlen, Sq == Sk), or NULL */
+  int64_t q_stride[3];    /* batch, seq, head strides (elements) */
+  int64_t k_stride[3];
+  int64_t v_stride[3];
+  int64_t o_stride[3];
+  int64_t bias_stride[3]; /* batch, head, row strides; 0 = broadcast */
+  int32_t batch, heads_q, heads_kv, seqlen_q, seqlen_k, head_dim;
+  int32_t lse_row_stride;
+  int32_t causal;         /* bottom-right aligned causal mask */
+  int32_t dtype;          /* FA2_F16 or FA2_BF16 (q, k, v, o) */
+  int32_t bias_dtype;     /* FA2_F16, FA2_BF16 or FA2_F32 when bias != NULL */
+  float softmax_scale;
+  float dropout_p;        /* 0 <= p < 1 */
+  uint64_t dropout_seed;  /* Philox4x32-10 key, identical to Triton's tl.rand */
+} fa2_fwd_args;
+
+/* Backward: dQ, dK, dV of the forward above (dropout_p must be 0, as in the reference,
+ * /root/reference/src/utils.py:80-88).  dK/dV are written with heads_kv heads: the GQA
+ * group sum is done in fp32 inside the kernel. */
+typedef struct fa2_bwd_args {
+  const void* q;
+  const void* k;
+  const void* v;
+  const void* o;
+  const void* dout;       /* dO, [B, Sq, Hq, D] */
+  const float* lse;       /* as written by fa2_fwd */
+  float* delta;           /* workspace [B, Hq, lse_row_stride] fp32 (rowsum(O * dO)) */
+  void* dq;               /* [B, Sq, Hq, D] in dq_dtype */
+  void* dk;               /* [B, Sk, Hkv, D] in dtype */
+  void* dv;               /* [B, Sk, Hkv, D] in dtype */
+  const void* bias;
+  const int32_t* cu_seqlens;
+  int64_t q_stride[3];
+  int64_t k_stride[3];
+  int64_t v_stride[3];
+  int64_t o_stride[3];
+  int64_t do_stride[3];
+  int64_t dq_stride[3];
+  int64_t dk_stride[3];
+  int64_t dv_stride[3];
+  int64_t bias_stride[3];
+  int32_t batch, heads_q, heads_kv, seqlen_q, seqlen_k, head_dim;
+  int32_t lse_row_stride;
+  int32_t causal;
+  int32_t dtype;
+  int32_t bias_dtype;
+  int32_t dq_dtype;       /* dtype, or FA2_F32 */
+  float softmax_scale;
+  float dropout_p;
+  uint64_t dropout_seed;
+} fa2_bwd_args;
+
+int fa2_fwd(const fa2_fwd_args* args, void* stream);
+int fa2_bwd(const fa2_bwd_args* args, void* stream);
+
+/* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,
+ * row stride mask_row_stride bytes).  Replaces attention_mask.sum(1).cumsum(0) and the
+ * .item() syncs of the reference callers (src/forward/caller.py:48-50, src/utils.py:8-17). */
+int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch,
+                             int32_t seqlen, int32_t* cu_seqlens, void* stream);
+
+const char* fa2_last_error(void);
+int fa2_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FA2_AMD_H */

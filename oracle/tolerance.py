@@ -1,0 +1,54 @@
+"""The reference tests' acceptance rule (TEST INFRASTRUCTURE ONLY).
+
+Restates compare_results_fa (/root/reference/tests/utils.py:68-142): the error of the
+operator under test against the fp32 oracle must be within a small multiple of the error a
+plain low-precision PyTorch implementation (oracle with upcast=False, reorder_ops=True) makes:
+  output : max|out - ref| <= 2 * max|pt - ref| + 5e-5          (:93)
+  dQ, dK : max|g - ref|   <= 3 * max|g_pt - ref| + 1e-5        (:127, :130)
+  dV     : same bound, or sum|dv - ref| < 1e-4 (with a warning) (:131-140)
+"""
+import warnings
+from typing import Optional, Sequence
+
+import torch
+from torch import Tensor
+
+
+def _maxdiff(a: Tensor, b: Tensor) -> float:
+    return (a.float() - b.float()).abs().max().item() if a.numel() else 0.0
+
+
+def check_fa_tolerance(
+    q: Tensor,
+    k: Tensor,
+    v: Tensor,
+    do: Optional[Tensor],
+    out: Tensor,
+    out_ref: Tensor,
+    out_pt: Tensor,
+    out_error_mul: float = 2.0,
+    out_error_bias: float = 5e-5,
+    grad_error_mul: float = 3.0,
+    grad_error_bias: float = 1e-5,
+    grads: Optional[Sequence[Tensor]] = None,
+) -> dict:
+    """Raise AssertionError when the rule above is violated; return the measured errors."""
+    report = {"out": _maxdiff(out, out_ref), "out_pt": _maxdiff(out_pt, out_ref)}
+    assert report["out"] <= out_error_mul * report["out_pt"] + out_error_bias, f"Output {report}"
+    if do is None:
+        return report
+    if grads is None:
+        grads = torch.autograd.grad(out, (q, k, v), do, retain_graph=True)
+    g_ref = torch.autograd.grad(out_ref, (q, k, v), do, retain_graph=True)
+    g_pt = torch.autograd.grad(out_pt, (q, k, v), do, retain_graph=True)
+    for name, g, gr, gp in zip(("dq", "dk", "dv"), grads, g_ref, g_pt):
+        err, err_pt = _maxdiff(g, gr), _maxdiff(gp, gr)
+        report[name], report[name + "_pt"] = err, err_pt
+        ok = err <= grad_error_mul * err_pt + grad_error_bias
+        if not ok and name == "dv":
+            total = (g.float() - gr.float()).abs().sum().item()
+            if total < 1e-4:
+                warnings.warn(f"small dV errors summing to {total}", stacklevel=2)
+                ok = True
+        assert ok, f"Gradient of {name}: {report}"
+    return report

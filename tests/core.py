@@ -1,0 +1,78 @@
+"""GPU parity harness -- the reference's tests/core.py + tests/utils.py, Triton-free.
+
+Mirrors /root/reference/tests/core.py:10-78 (_test_core_fn) and the generators of
+/root/reference/tests/utils.py: generate_test_data (:9-26, seed 0, N(0, 0.5) Q/K/V, N(0, 1) dO),
+generate_attention_mask (:40-56, right padding, one full row), generate_dropout_seed_and_mask
+(:169-207, here with the torch Philox of oracle/philox.py instead of a Triton kernel) and the
+acceptance rule compare_results_fa (:68-142, oracle/tolerance.py).  The oracle is run on the
+same device tensors, fp32-upcast ("ref") and in the input dtype with reordered ops ("pt").
+"""
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from oracle.philox import dropout_keep_mask_torch
+from oracle.reference import attention_reference
+from oracle.tolerance import check_fa_tolerance
+
+
+def generate_test_data(batch_size, nheads_q, nheads_kv, seqlen_q, seqlen_k, head_dim, dtype, seed=0, device="cuda"):
+    torch.manual_seed(seed)
+    q = torch.empty((batch_size, seqlen_q, nheads_q, head_dim), dtype=dtype, device=device).normal_(0.0, 0.5)
+    k = torch.empty((batch_size, seqlen_k, nheads_kv, head_dim), dtype=dtype, device=device).normal_(0.0, 0.5)
+    v = torch.empty((batch_size, seqlen_k, nheads_kv, head_dim), dtype=dtype, device=device).normal_(0.0, 0.5)
+    do = torch.randn_like(q)
+    return q.requires_grad_(), k.requires_grad_(), v.requires_grad_(), do
+
+
+def generate_attention_mask(x: Tensor) -> Tensor:
+    """Random right padding per batch row, one row unpadded (reference tests/utils.py:40-56)."""
+    mask = torch.ones(size=x.shape[:2], dtype=torch.bool, device=x.device)
+    if x.size(1) == 1:
+        return mask
+    padding = torch.randint(low=0, high=x.size(1) - 1, size=(x.size(0),)).tolist()
+    padding[torch.randint(low=0, high=x.size(0), size=(1,)).item()] = 0
+    for i, pad in enumerate(padding):
+        if pad:
+            mask[i, -pad:] = False
+    return mask
+
+
+def generate_dropout_seed_and_mask(dropout_p, q, k, attention_mask) -> Tuple[Optional[int], Optional[Tensor]]:
+    if dropout_p == 0:
+        return None, None
+    seed = torch.randint(low=0, high=2**32, size=(1,)).item()
+    assert attention_mask is None, "dropout + padding mask is not exercised by the reference tests"
+    b, sq, hq, _ = q.shape
+    return seed, dropout_keep_mask_torch(seed, dropout_p, b, hq, sq, k.size(1), device=q.device)
+
+
+def run_case(
+    batch_size: int,
+    nheads_q: int,
+    nheads_kv: int,
+    seqlen_q: int,
+    seqlen_k: int,
+    head_dim: int,
+    causal: bool,
+    dropout_p: float,
+    use_attention: bool,
+    use_bias: bool,
+    dtype: torch.dtype,
+    forward_only: bool,
+) -> dict:
+    from fa2_triton_amd import flash_attn_func
+
+    q, k, v, do = generate_test_data(batch_size, nheads_q, nheads_kv, seqlen_q, seqlen_k, head_dim, dtype)
+    attn_mask = generate_attention_mask(q) if use_attention else None
+    attn_bias = torch.rand(size=(1, 1, seqlen_q, seqlen_k), dtype=dtype, device=q.device) if use_bias else None
+    dropout_seed, dropout_mask = generate_dropout_seed_and_mask(dropout_p, q, k, attn_mask)
+    common = dict(query_padding_mask=attn_mask, key_padding_mask=attn_mask, attn_bias=attn_bias,
+                  dropout_p=dropout_p, dropout_mask=dropout_mask, causal=causal)
+    out_ref = attention_reference(q, k, v, **common)
+    out_pt = attention_reference(q, k, v, upcast=False, reorder_ops=True, **common)
+    out = flash_attn_func(q, k, v, attention_mask=attn_mask, attention_bias=attn_bias, dropout_p=dropout_p,
+                          causal=causal, softmax_scale=None, dropout_seed=dropout_seed)
+    assert out.shape == q.shape and out.dtype == q.dtype
+    return check_fa_tolerance(q, k, v, None if forward_only else do, out, out_ref, out_pt)
