@@ -1,0 +1,217 @@
+"""Benchmark: attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16 and % of MFMA peak.
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on): per GPU
+B=8 H=32 S=4096 D=128 bf16, causal, forward + backward through the autograd op
+`fa2_triton_amd.flash_attn_func` on synthetic N(0, 0.5) inputs resident in HBM.  One step =
+one forward + one backward of that batch.  With N GPUs each rank runs its own B=8 shard
+(configs[3]: B=64 over 8 GPUs), no collectives on the data path (weak scaling).
+
+FLOPs are algorithmic: fwd = 4 B H S^2 D / 2 (causal), bwd = 2.5 fwd.
+
+Besides the step time, the forward kernel (the north-star kernel) and the backward launch
+(delta + dK/dV + dQ kernels) are timed with HIP events on the stream they run on, giving the
+`roofline` object, and rank 0 times the CPU oracle (oracle/reference.py, fp32, torch CPU
+threads) on a bounded slice of the same workload for `cpu_baseline`.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+METRIC = "attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16; % of MFMA peak"
+
+
+def attn_flops(b, h, sq, sk, d, causal):
+    f = 4.0 * b * h * sq * sk * d
+    return f * 0.5 if causal else f
+
+
+def cpu_baseline(b, h, s, d, causal, budget_s=20.0):
+    """Time the fp32 oracle (fwd+bwd) on the host; slice of the same workload."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle.reference import attention_reference
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    heads = h
+    # bound memory/time: one batch element, shrink heads until a rep fits the budget
+    best = None
+    while heads >= 1:
+        q = (torch.randn(1, s, heads, d, generator=g) * 0.5).requires_grad_()
+        k = (torch.randn(1, s, heads, d, generator=g) * 0.5).requires_grad_()
+        v = (torch.randn(1, s, heads, d, generator=g) * 0.5).requires_grad_()
+        do = torch.randn(1, s, heads, d, generator=g)
+        t0 = time.perf_counter()
+        out = attention_reference(q, k, v, causal=causal)
+        torch.autograd.grad(out, (q, k, v), do)
+        dt = time.perf_counter() - t0
+        best = (heads, dt)
+        if dt <= budget_s:
+            break
+        heads //= 2
+    heads, dt = best
+    flops = 3.5 * attn_flops(1, heads, s, s, d, causal)
+    return {
+        "value": flops / dt / 1e12,
+        "unit": "TFLOP/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle fp32 fwd+bwd, B=1 H={heads} S={s} D={d} causal={causal} (slice of the workload), {dt:.2f} s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--heads", type=int, default=32)
+    ap.add_argument("--seqlen", type=int, default=4096)
+    ap.add_argument("--head-dim", type=int, default=128)
+    ap.add_argument("--no-causal", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    from fa2_triton_amd import flash_attn_func
+    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.forward import _flash_attn_forward
+
+    b, h, s, d = args.batch, args.heads, args.seqlen, args.head_dim
+    causal = not args.no_causal
+    dtype = torch.bfloat16
+    torch.manual_seed(1234 + rank)
+    q = torch.empty(b, s, h, d, device=device, dtype=dtype).normal_(0, 0.5).requires_grad_()
+    k = torch.empty(b, s, h, d, device=device, dtype=dtype).normal_(0, 0.5).requires_grad_()
+    v = torch.empty(b, s, h, d, device=device, dtype=dtype).normal_(0, 0.5).requires_grad_()
+    do = torch.randn(b, s, h, d, device=device, dtype=dtype)
+
+    def step():
+        out = flash_attn_func(q, k, v, causal=causal)
+        torch.autograd.grad(out, (q, k, v), do)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    f_fwd = attn_flops(b, h, s, s, d, causal)
+    f_step = 3.5 * f_fwd
+    total = f_step * args.steps * world
+    value = total / elapsed / 1e12
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- per-launch timing with HIP events on the launch stream ---------------------------
+    reps = max(5, args.steps)
+    stream = torch.cuda.current_stream(device)
+    with torch.no_grad():
+        o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        ev[1].record(stream)
+        for _ in range(reps):
+            _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None)
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+    t_fwd = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    t_bwd = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+    fwd_tf = f_fwd / t_fwd / 1e12
+    bwd_tf = 2.5 * f_fwd / t_bwd / 1e12
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(b, h, s, d, causal)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic N(0,0.5) Q/K/V, N(0,1) dO, resident in HBM",
+        "config": {
+            "workload": f"B={b} H={h} S={s} D={d} bf16 {'causal' if causal else 'non-causal'} fwd+bwd per GPU "
+                        "(BASELINE.json configs[2]; configs[3] when batch-sharded over 8 GPUs)",
+            "global_batch": b * world,
+            "seq_len": s,
+            "heads": h,
+            "head_dim": d,
+            "causal": causal,
+            "parallelism": f"batch-sharded x{world}, independent per-GPU launches, no collectives",
+        },
+        "fwd_tflops": round(fwd_tf, 2),
+        "bwd_tflops": round(bwd_tf, 2),
+        "fwd_ms": round(t_fwd * 1e3, 4),
+        "bwd_ms": round(t_bwd * 1e3, 4),
+        "pct_of_peak_fwd": round(100 * fwd_tf / PEAK_TFLOPS, 2),
+        "pct_of_peak_fwd_bwd": round(100 * value / world / PEAK_TFLOPS, 2),
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "fa2::fwd_kernel (forward, one launch per call)",
+            "achieved": round(fwd_tf, 2),
+            "peak": PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(fwd_tf / PEAK_TFLOPS, 4),
+            "traffic": None,
+        },
+        "roofline_bwd": {
+            "bound": "mfma",
+            "kernel": "delta + dkdv + dq launches of one fa2_bwd call",
+            "achieved": round(bwd_tf, 2),
+            "peak": PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(bwd_tf / PEAK_TFLOPS, 4),
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,11 +26,19 @@ def _keep(case) -> bool:
     return zlib.crc32(repr(case).encode()) % STRIDE == 0
 
 
+def case_id(c) -> str:
+    dt = "f16" if c[0] == torch.float16 else "bf16"
+    sw, att, bias = c[4]
+    mode = ("swap" if sw else "") + ("mask" if att else "") + ("bias" if bias else "") or "plain"
+    heads = c[6] if isinstance(c[6], tuple) else (c[6], c[6])
+    return f"{dt}-p{c[1]}-{'causal' if c[2] else 'full'}-d{c[3]}-{mode}-s{c[5][0]}x{c[5][1]}-h{heads[0]}x{heads[1]}"
+
+
 SELECTED = [c for c in GRID if _keep(c)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,dropout_p,causal,head_dim,mode,seqlens,heads,batch_size", SELECTED)
+@pytest.mark.parametrize("dtype,dropout_p,causal,head_dim,mode,seqlens,heads,batch_size", SELECTED, ids=[case_id(c) for c in SELECTED])
 def test_fwd_bwd(dtype, dropout_p, causal, head_dim, mode, seqlens, heads, batch_size):
     swap_seqlens, use_attention, use_bias = mode
     seqlen_q, seqlen_k = seqlens
