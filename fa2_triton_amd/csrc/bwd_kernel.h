@@ -13,6 +13,8 @@
 // Differences by design: the GQA group sum of dK/dV is done in fp32 registers inside
 // dkdv_kernel (the reference sums bf16/fp16 tensors on the host), dQ is written directly in
 // the requested dtype, and padded varlen rows are handled in place (no pack/unpack).
+#include <type_traits>
+
 #include "common.h"
 #include "fa2_internal.h"
 
@@ -54,22 +56,27 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 
 // ---------------------------------------------------------------------------------------------
 // dK, dV: one workgroup = 4 waves = 128 keys of one (batch, kv-head); wave w owns keys
-// n0 + 32 w + (lane & 31).  K and V stay in VGPRs as the B operands of S = Q K^T and
-// dP = dO V^T; the workgroup sweeps the q-heads of its GQA group and 32-row query tiles
-// (Q and dO staged in LDS, double buffered).  Per tile and wave:
-//   S[q][key], dP[q][key]   8 + 8 MFMA (A = Q / dO row fragments from LDS)
+// n0 + 32 w + (lane & 31).  K stays in VGPRs (B operand of S = Q K^T), the workgroup's V rows
+// sit in LDS (B operand of dP = dO V^T, read as row fragments), and the workgroup sweeps the
+// q-heads of its GQA group and 32-row query tiles (Q, dO, LSE2 and delta staged in LDS by
+// LDS-DMA, double buffered).  Per tile and wave:
+//   S[q][key], dP[q][key]   8 + 8 MFMA (A = Q / dO row fragments)
 //   dV^T[d][key] += dO^T P  NDT*2 MFMA (A = dO^T via ds_read_b64_tr_b16, B = P registers)
 //   dK^T[d][key] += Q^T dS  NDT*2 MFMA
+// dK/dV accumulate the whole GQA group in fp32 and are rounded once.  <= 256 VGPRs, so two
+// workgroups share a CU (DT <= 128).
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
-__global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NT = 256;
   constexpr int BNK = 128;          // keys per workgroup
   constexpr int BMQ = 32;           // query rows per tile
   constexpr int KS = DT / 16;
   constexpr int NDT = DT / 32;
-  constexpr int TILE = BMQ * DT * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // Q0 dO0 Q1 dO1
+  constexpr int VT = BNK * DT * 2;  // V tile bytes
+  constexpr int QT = BMQ * DT * 2;  // Q (or dO) tile bytes
+  constexpr int ST = 2 * BMQ * 4;   // LSE2 + delta rows of a tile
+  __shared__ __attribute__((aligned(16))) char smem[VT + 4 * QT + 2 * ST];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -83,23 +90,14 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
   const int diag = Lk - Lq;
   const int kw0 = n0 + 32 * w;   // first key of this wave
   const int kj = kw0 + r32;      // this lane's key
+  const bool kval = kj < Lk;
   const float scale = p.softmax_scale, scale2 = scale * kLog2e;
+  const float sc = BIAS ? 1.f : scale2;
 
-  // K / V fragments: B operands, K[kj][16 ks + 8 hh + j]
-  u32x4 kf[KS], vf[KS];
-  {
-    const bool kval = kj < Lk;
-    const uint16_t* krow = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2] + (int64_t)(kval ? kj : 0) * p.k_stride[1];
-    const uint16_t* vrow = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2] + (int64_t)(kval ? kj : 0) * p.v_stride[1];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      kf[ks] = load_row_frag<ALIGNED>(krow, 16 * ks + 8 * hh, D, kval);
-      vf[ks] = load_row_frag<ALIGNED>(vrow, 16 * ks + 8 * hh, D, kval);
-    }
-  }
-  f32x16 dk[NDT], dv[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+  char* Vs = smem;
+  auto qt = [&](int buf) { return smem + VT + buf * 2 * QT; };
+  auto ot = [&](int buf) { return smem + VT + QT + buf * 2 * QT; };
+  auto st = [&](int buf) { return smem + VT + 4 * QT + buf * ST; };
 
   // query tiles: causal -> the first row that sees key n0 is n0 - diag
   int m_begin = 0;
@@ -107,8 +105,6 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
   const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
   const int total = n_mt * G;  // (q-head, tile) steps
 
-  auto qt = [&](int buf) { return smem + buf * 2 * TILE; };
-  auto ot = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
   auto stage = [&](int step, int buf) {
     const int g = step / n_mt, mt = step - g * n_mt;
     const int hq = hkv * G + g;
@@ -117,10 +113,97 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
     stage_tile<DT, BMQ, NT, ALIGNED>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
     stage_tile<DT, BMQ, NT, ALIGNED>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
+    if (w == 0) {  // LSE2 rows -> lanes 0..31, delta rows -> lanes 32..63 (one 256-byte piece)
+      const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m + r32;
+      const float* src = hh ? p.delta + srow : p.lse + srow;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)st(buf), 4, 0, 0);
+    }
   };
-  if (total > 0) stage(0, 0);
+
+  u32x4 kf[KS];
+  {
+    const uint16_t* krow = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2] + (int64_t)(kval ? kj : 0) * p.k_stride[1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = load_row_frag<ALIGNED>(krow, 16 * ks + 8 * hh, D, kval);
+  }
+  if (total > 0) {
+    const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
+    stage_tile<DT, BNK, NT, ALIGNED>(Vs, vg, p.v_stride[1], n0, Lk, D, tid);
+    stage(0, 0);
+  }
+  f32x16 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+
+  // rows q of this lane's key that survive the masks: q_lo <= q < Lq (none if the key is padding)
+  const int q_lo = CAUSAL ? max(kj - diag, 0) : 0;
+  const int q_hi = kval ? Lq : -1;
+
+  auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BMQ>(Q, 0, r32, 2 * ks + hh), kf[ks], s);
+    __builtin_amdgcn_sched_barrier(0);  // keep each phase's fragment loads inside the phase
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      dp = E::mfma(lds_row_frag<DT, BMQ>(O, 0, r32, 2 * ks + hh), lds_row_frag<DT, BNK>(Vs, 32 * w, r32, 2 * ks + hh), dp);
+    __builtin_amdgcn_sched_barrier(0);
+    // rows of register i: m + (i & 3) + 8 (i >> 2) + 4 hh
+    const int lo = q_lo - m - 4 * hh, hi = q_hi - m - 4 * hh;
+    u32x4 pp[2], dsp[2];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 l4 = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh));
+      const f32x4 d4 = *(const f32x4*)(S + 4 * BMQ + 4 * (8 * g4 + 4 * hh));
+      float pv[4], dsv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * g4 + j;
+        const int o = j + 8 * g4;
+        float x = s[i];
+        if (BIAS) {
+          const int qr = m + o + 4 * hh;
+          const int qc = qr < Lq ? qr : Lq - 1;
+          const int kc = kval ? kj : Lk - 1;
+          x = fmaf(x, scale2, kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                                           (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype));
+        }
+        float pr = __builtin_amdgcn_exp2f(fmaf(x, sc, -l4[j]));
+        if (MASK) pr = (o >= lo && o < hi) ? pr : 0.f;
+        pv[j] = pr;
+        dsv[j] = pr * (dp[i] - d4[j]);  // softmax_scale is applied to dK once, at the end
+      }
+      pp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(pv[0], pv[1]);
+      pp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(pv[2], pv[3]);
+      dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
+      dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        dv[dt] = E::mfma(lds_tr_frag<DT, BMQ>(O, 16 * sp, 32 * dt, lane), pp[sp], dv[dt]);
+        dk[dt] = E::mfma(lds_tr_frag<DT, BMQ>(Q, 16 * sp, 32 * dt, lane), dsp[sp], dk[dt]);
+      }
+      if (dt & 1) __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
+    }
+  };
+
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (ALIGNED && D < DT && total > 0) {
+    // dP = dO V^T reads both operands from LDS, whose clamped staging repeats the last real
+    // chunk in the padding columns: zero V's padding once so those columns contribute nothing.
+    constexpr int kChunks = DT / 8;
+    const int c0 = D >> 3;
+    for (int idx = tid; idx < BNK * kChunks; idx += NT) {
+      const int r = idx / kChunks, c = idx % kChunks;
+      if (c >= c0) *(u32x4*)(Vs + Tile<DT, BNK>::off(r, c)) = u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+  }
 
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
@@ -128,65 +211,14 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
     const int g = step / n_mt, mt = step - g * n_mt;
     const int hq = hkv * G + g;
     const int m = m_begin + mt * BMQ;
-    const char* Q = qt(cur);
-    const char* O = ot(cur);
-
-    // does any (query, key) of this wave survive the masks?
-    const bool active = kw0 < Lk && (!CAUSAL || kw0 <= m + BMQ - 1 + diag);
-    if (active) {
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT>(Q, r32, 2 * ks + hh), kf[ks], s);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT>(O, r32, 2 * ks + hh), vf[ks], dp);
-
-      // row statistics of the 16 query rows held in registers: rows m + 8 g4 + 4 hh + (0..3)
-      const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m;
-      f32x4 lse4[4], del4[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        lse4[g4] = *(const f32x4*)(p.lse + srow + 8 * g4 + 4 * hh);
-        del4[g4] = *(const f32x4*)(p.delta + srow + 8 * g4 + 4 * hh);
-      }
-      const bool need_mask = (kw0 + 31 >= Lk) || (m + BMQ > Lq) || (CAUSAL && kw0 + 31 > m + diag);
-      u32x4 pp[2], dsp[2];
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        float pv[8], dsv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int i = 8 * sp + j;
-          const int qrow = m + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          float x = s[i] * scale2;
-          if (BIAS) {
-            const int qc = qrow < Lq ? qrow : Lq - 1;
-            const int kc = kj < Lk ? kj : Lk - 1;
-            x += kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
-                                                (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
-          }
-          float pr = __builtin_amdgcn_exp2f(x - lse4[i >> 2 & 3][i & 3]);
-          if (need_mask) {
-            bool ok = kj < Lk && qrow < Lq;
-            if (CAUSAL) ok = ok && (kj <= qrow + diag);
-            pr = ok ? pr : 0.f;
-          }
-          pv[j] = pr;
-          dsv[j] = pr * (dp[i] - del4[i >> 2 & 3][i & 3]) * scale;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pp[sp][j] = E::pack2(pv[2 * j], pv[2 * j + 1]);
-          dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
-        }
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp) {
-          dv[dt] = E::mfma(lds_tr_frag<DT>(O, 16 * sp, 32 * dt, lane), pp[sp], dv[dt]);
-          dk[dt] = E::mfma(lds_tr_frag<DT>(Q, 16 * sp, 32 * dt, lane), dsp[sp], dk[dt]);
-        }
-      }
+    // wave-uniform tile class
+    const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
+    const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);
+    if (!dead) {
+      if (need_mask)
+        body(std::true_type{}, qt(cur), ot(cur), st(cur), hq, m);
+      else
+        body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -194,7 +226,6 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
 
   // ---- store dK, dV (kv heads; fp32 group sum rounded once) ----------------------------
   if (kj < p.seqlen_k) {
-    const bool kval = kj < Lk;
     uint16_t* dkrow = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kj * p.dk_stride[1];
     uint16_t* dvrow = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kj * p.dv_stride[1];
 #pragma unroll
@@ -205,7 +236,7 @@ __global__ void __launch_bounds__(256, 1) dkdv_kernel(const fa2_bwd_args p) {
         float a[4], c[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          a[j] = kval ? dk[dt][4 * g4 + j] : 0.f;
+          a[j] = kval ? dk[dt][4 * g4 + j] * scale : 0.f;
           c[j] = kval ? dv[dt][4 * g4 + j] : 0.f;
         }
         if (ALIGNED) {
@@ -295,26 +326,26 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int cur = it & 1;
-    const int n0 = it * BN;
-    if (it + 1 < ntiles) {
-      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
-      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
-    }
-    const char* K = kt(cur);
-    const char* V = vt(cur);
+  // key kj visible to this lane's row iff kj < lim_lane (0 for padded rows)
+  const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + diag + 1) : Lk);
+  const float sc = BIAS ? 1.f : scale2;
+  const float nlse = -lse_i;
+
+  // one 64-key tile: S^T and dP^T for both 32-key halves first, then the softmax-gradient
+  // VALU of each half beside the other half's MFMAs, then dQ^T += K^T dS^T.
+  auto tile = [&](auto mask_c, const char* K, const char* V, int n0) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int rel = lim_lane - n0 - 4 * hh;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int kt0 = n0 + 32 * t;
-      const bool active = kt0 < Lk && (!CAUSAL || kt0 <= mw0 + 31 + diag);
-      if (!active) continue;
+      if (MASK && !(n0 + 32 * t < Lk && (!CAUSAL || n0 + 32 * t <= mw0 + 31 + diag))) continue;
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT>(K, 32 * t + r32, 2 * ks + hh), qf[ks], s);
+      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, 2 * ks + hh), qf[ks], s);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT>(V, 32 * t + r32, 2 * ks + hh), of[ks], dp);
-      const bool need_mask = (kt0 + 31 >= Lk) || !qvalid || (CAUSAL && kt0 + 31 > mw0 + diag) || (mw0 + 31 >= Lq);
+      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, 2 * ks + hh), of[ks], dp);
+      __builtin_amdgcn_sched_barrier(0);
       u32x4 dsp[2];
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
@@ -322,30 +353,47 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int i = 8 * sp + j;
-          const int kj = kt0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          float x = s[i] * scale2;
+          const int o = 32 * t + (i & 3) + 8 * (i >> 2);
+          float x = s[i];
           if (BIAS) {
+            const int kj = n0 + o + 4 * hh;
             const int kc = kj < Lk ? kj : Lk - 1;
             const int qc = qvalid ? qi : 0;
-            x += kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
-                                                (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
+            x = fmaf(x, scale2, kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                                             (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype));
           }
-          float pr = __builtin_amdgcn_exp2f(x - lse_i);
-          if (need_mask) {
-            bool ok = kj < Lk && qvalid;
-            if (CAUSAL) ok = ok && (kj <= qi + diag);
-            pr = ok ? pr : 0.f;
-          }
-          dsv[j] = pr * (dp[i] - del_i) * scale;
+          float pr = __builtin_amdgcn_exp2f(fmaf(x, sc, nlse));
+          if (MASK) pr = o < rel ? pr : 0.f;
+          dsv[j] = pr * (dp[i] - del_i);  // softmax_scale is applied to dQ once, at the end
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
+      for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp)
-          acc[dt] = E::mfma(lds_tr_frag<DT>(K, 32 * t + 16 * sp, 32 * dt, lane), dsp[sp], acc[dt]);
+          acc[dt] = E::mfma(lds_tr_frag<DT, BN>(K, 32 * t + 16 * sp, 32 * dt, lane), dsp[sp], acc[dt]);
+        if (dt & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const int n0 = it * BN;
+    if (it + 1 < ntiles) {
+      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
+      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
+    }
+    const bool dead = CAUSAL && (n0 > mw0 + 31 + diag);
+    const bool need_mask = (n0 + BN > Lk) || (mw0 + 31 >= Lq) || (CAUSAL && n0 + BN - 1 > mw0 + diag);
+    if (!dead) {
+      if (need_mask)
+        tile(std::true_type{}, kt(cur), vt(cur), n0);
+      else
+        tile(std::false_type{}, kt(cur), vt(cur), n0);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -363,7 +411,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
         const int d0 = 32 * dt + 8 * g4 + 4 * hh;
         float a[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = ok ? acc[dt][4 * g4 + j] : 0.f;
+        for (int j = 0; j < 4; ++j) a[j] = ok ? acc[dt][4 * g4 + j] * scale : 0.f;
         if (DQF32) {
           float* r = (float*)row;
           if (ALIGNED) {

@@ -8,9 +8,9 @@
 //   are per-lane scalars and the probability accumulator is already the B operand of the next
 //   product (the k order inside a 16-wide k-step is then 8(j>>2) + 4h + (j&3); the other
 //   operand is read in that same order through ds_read_b64_tr_b16).
-// * LDS tiles are [rows][DT] 16-bit elements with 16-byte chunks XOR-swizzled per row so that
-//   both 16-byte row reads (ds_read_b128, A/B fragments) and 4-row transposed reads
-//   (ds_read_b64_tr_b16) are bank-conflict free (swizzle below).
+// * LDS tiles are stored d-tile major (32-column sub-tiles, 64-byte rows, 16-byte chunks
+//   XOR-swizzled) so that 16-byte row reads (ds_read_b128, A/B fragments) and 4-row transposed
+//   reads (ds_read_b64_tr_b16) are both bank-conflict free (layout below).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -99,43 +99,47 @@ FA2_DEV f32x16 zero16() {
 }
 
 // ---------------------------------------------------------------------------------------------
-// LDS tile layout.  A tile is `rows` x DT 16-bit elements (DT in {32, 64, 128, 256}), row
-// pitch 2*DT bytes, 16-byte chunk c of row r stored at chunk c ^ swz(r).  The swizzle keeps
-//  (a) a ds_read_b128 lane group (16 lanes, 16 distinct rows, one chunk each) on 16 distinct
-//      16-byte slots of the 256-byte bank row, and
-//  (b) a ds_read_b64_tr_b16 half wave (4 consecutive rows x 4 consecutive chunks) on 16
-//      distinct slots as well.
-template <int DT>
+// LDS tile layout ("d-tile major").  A tile of ROWS x DT 16-bit elements is stored as DT/32
+// sub-tiles of ROWS x 32 columns; each sub-tile row is 64 bytes (four 16-byte chunks) and
+// chunk cc of row r sits at cc ^ ((r >> 2) & 3).  With this image
+//  (a) a ds_read_b128 lane group (16 lanes, 16 distinct rows, one chunk each) hits 16 distinct
+//      16-byte bank slots, and
+//  (b) a ds_read_b64_tr_b16 half wave (4 consecutive rows x 64 bytes of one sub-tile) covers
+//      one whole 256-byte bank row,
+// so both are conflict free, and -- unlike an XOR over 256-byte rows -- every read of a
+// (sub-tile, row block) differs from the lane's base address by a compile-time constant, so the
+// loops keep only a couple of address registers per tile (ds_read offset immediates).
+template <int DT, int ROWS>
 struct Tile {
-  static constexpr int kRowBytes = DT * 2;
   static constexpr int kChunks = DT / 8;
-  FA2_DEV static int swz(int r) {
-    if constexpr (DT == 32) return (r >> 2) & 3;
-    else if constexpr (DT == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
-    else return ((r & 3) << 2) | ((r >> 2) & 3);
-  }
-  // byte offset of chunk c of row r
-  FA2_DEV static int off(int r, int c) { return r * kRowBytes + ((c ^ swz(r)) << 4); }
+  static constexpr int kSub = ROWS * 64;  // bytes per 32-column sub-tile
+  // byte offset of global chunk c (8 columns) of row r
+  FA2_DEV static int off(int r, int c) { return (c >> 2) * kSub + r * 64 + (((c & 3) ^ ((r >> 2) & 3)) << 4); }
 };
 
-// 16-byte row fragment: row r, chunk c  (A or B operand of a 32x32x16 MFMA).
-template <int DT>
-FA2_DEV u32x4 lds_row_frag(const char* tile, int r, int c) {
-  return *(const u32x4*)(tile + Tile<DT>::off(r, c));
+// 16-byte row fragment: row row0 + r32 (row0 % 16 == 0), chunk c  (A or B operand of a
+// 32x32x16 MFMA: element j = column 8c + j).
+template <int DT, int ROWS>
+FA2_DEV u32x4 lds_row_frag(const char* tile, int row0, int r32, int c) {
+  const int off = (c >> 2) * Tile<DT, ROWS>::kSub + (row0 + r32) * 64 + (((c & 3) ^ ((r32 >> 2) & 3)) << 4);
+  return *(const u32x4*)(tile + off);
 }
 
-// Transposed fragment for the operand whose k index runs over tile ROWS:
-// element j of lane (r32 = l & 31, h = l >> 5) = tile[row0 + 8 (j >> 2) + 4 h + (j & 3)][col0 + r32]
-// (the permuted k order matching a C-layout accumulator reused as the other operand).
-template <int DT>
+// Transposed fragment for the operand whose k index runs over tile ROWS (row0 % 16 == 0,
+// col0 % 32 == 0): element j of lane (r32 = l & 31, h = l >> 5) is
+//   tile[row0 + 8 (j >> 2) + 4 h + (j & 3)][col0 + r32]
+// i.e. the permuted k order of a C-layout accumulator reused as the other MFMA operand.
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3 of its
+// block and receives column (lane & 15) of the 4 rows.
+template <int DT, int ROWS>
 FA2_DEV u32x4 lds_tr_frag(const char* tile, int row0, int col0, int lane) {
   const int i = lane & 15, g = lane >> 4, h = lane >> 5;
-  const int col = col0 + 16 * (g & 1) + 4 * (i & 3);
-  const int c = col >> 3, half = (col >> 2) & 1;
-  const int ra = row0 + 4 * h + (i >> 2);
-  const int rb = ra + 8;
-  const lds_char* pa = (const lds_char*)(tile + Tile<DT>::off(ra, c) + half * 8);
-  const lds_char* pb = (const lds_char*)(tile + Tile<DT>::off(rb, c) + half * 8);
+  const int q = i >> 2, pq = i & 3;
+  const int cc = 2 * (g & 1) + (pq >> 1);
+  // rows row0 + 4h + q (first read) and row0 + 8 + 4h + q: (row >> 2) & 3 = h and h ^ 2
+  const int base = (col0 >> 5) * Tile<DT, ROWS>::kSub + (row0 + 4 * h + q) * 64 + 8 * (pq & 1);
+  const lds_char* pa = (const lds_char*)(tile + base + ((cc ^ h) << 4));
+  const lds_char* pb = (const lds_char*)(tile + base + 8 * 64 + ((cc ^ h ^ 2) << 4));
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
   u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
@@ -143,7 +147,7 @@ FA2_DEV u32x4 lds_tr_frag(const char* tile, int row0, int col0, int lane) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Global -> LDS tile staging.  `rows` rows starting at global row `row0` (row stride
+// Global -> LDS tile staging.  ROWS rows starting at global row `row0` (row stride
 // `row_stride` elements) of a [*, D] slice; rows >= row_end and columns >= D must not leak
 // NaN/Inf garbage into the MFMAs, so:
 //  ALIGNED (D % 8 == 0, 16-byte aligned rows): LDS-DMA 16-byte pieces
@@ -165,9 +169,11 @@ FA2_DEV void stage_tile(char* tile, const uint16_t* g, int64_t row_stride, int r
       const int wbase = (it * (NTHREADS / 64) + wave) * 64;  // first piece of this wave
       if (kPieces % NTHREADS != 0 && wbase >= kPieces) break;  // wave-uniform
       const int piece = wbase + lane;
-      const int pr = piece / kChunks;            // physical row
-      const int pc = piece % kChunks;            // physical chunk
-      const int c = pc ^ Tile<DT>::swz(pr);      // logical chunk stored there
+      const int sub = piece / (ROWS * 4);                      // 32-column sub-tile
+      const int within = piece % (ROWS * 4);
+      const int pr = within >> 2;                              // row
+      const int cc = (within & 3) ^ ((pr >> 2) & 3);           // logical chunk stored here
+      const int c = sub * 4 + cc;
       int grow = row0 + pr;
       grow = grow < row_end ? grow : row_end - 1;
       const int gc = c < dchunks ? c : dchunks - 1;
@@ -190,7 +196,7 @@ FA2_DEV void stage_tile(char* tile, const uint16_t* g, int64_t row_stride, int r
       u32x4 pk;
 #pragma unroll
       for (int j = 0; j < 4; ++j) pk[j] = uint32_t(vals[2 * j]) | (uint32_t(vals[2 * j + 1]) << 16);
-      *(u32x4*)(tile + Tile<DT>::off(r, c)) = pk;
+      *(u32x4*)(tile + Tile<DT, ROWS>::off(r, c)) = pk;
     }
   }
 }

@@ -12,6 +12,8 @@
 //   S^T[key][q] = K Q^T        16 MFMA 32x32x16 (A = K row frags from LDS, B = Q frags in VGPRs)
 //   softmax on the lane pair (l, l^32) holding one query row (16+16 keys per 32-key tile)
 //   O^T[d][q]  += V^T P^T      16 MFMA (A = V^T via ds_read_b64_tr_b16, B = P in registers)
+#include <type_traits>
+
 #include "common.h"
 #include "fa2_internal.h"
 
@@ -96,55 +98,51 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int cur = it & 1;
-    const int n0 = it * BN;
-    if (it + 1 < ntiles) {  // prefetch the next K/V tile into the other buffer
-      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
-      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
-    }
-    const char* K = kt(cur);
-    const char* V = vt(cur);
+  // Per-lane key limit: key kj is visible to this lane's row iff kj < lim_lane.
+  const int qw0 = m0 + w * 32;  // first row of this wave
+  const int lim_lane = CAUSAL ? min(Lk, qi + diag + 1) : Lk;
+  // Scores are kept raw (no bias) or already in base-2 units (bias): exp2 argument = x*sc - m.
+  const float sc = BIAS ? 1.f : scale2;
 
-    // ---- S^T = K Q^T for two 32-key halves --------------------------------------------
+  // One 64-key tile for this wave.  MASK selects the diagonal / tail variant at compile time so
+  // the common interior tile carries no per-element compare.
+  auto tile = [&](auto mask_c, const char* K, const char* V, int n0) {
+    constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       s[t] = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        s[t] = E::mfma(lds_row_frag<DT>(K, 32 * t + r32, 2 * ks + hh), qf[ks], s[t]);
+        s[t] = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, 2 * ks + hh), qf[ks], s[t]);
     }
-
-    // ---- scores in base 2, masks --------------------------------------------------------
-    // key of register i in half t: n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
-    const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > m0 + w * 32 + diag));
+    // register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
+    const int rel = lim_lane - n0 - 4 * hh;
     float mx = kNegInf;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        float x = s[t][i] * scale2;
+        const int o = 32 * t + (i & 3) + 8 * (i >> 2);
+        float x = s[t][i];
         if (BIAS) {
+          const int kj = n0 + o + 4 * hh;
           const int kc = kj < Lk ? kj : Lk - 1;
           const int qc = qi < Lq ? qi : 0;
-          x += kLog2e * load_bias(biasb, b * p.bias_stride[0] + hq * p.bias_stride[1] +
-                                             (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype);
+          x = fmaf(x, scale2, kLog2e * load_bias(biasb, b * p.bias_stride[0] + hq * p.bias_stride[1] +
+                                                          (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype));
         }
-        if (need_mask) {
-          bool ok = kj < Lk;
-          if (CAUSAL) ok = ok && (kj <= qi + diag);
-          x = ok ? x : kNegInf;
-        }
+        if (MASK) x = o < rel ? x : kNegInf;
         s[t][i] = x;
         mx = fmaxf(mx, x);
       }
     }
-    mx = half_max(mx);
+    mx = half_max(mx) * sc;
     const float m_new = fmaxf(m_run, mx);
     const float m_use = m_new == kNegInf ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+    // exact lazy rescale: skip the O pass when no row max of the wave moved
+    const bool rescale = !__all(m_new == m_run);
     m_run = m_new;
 
     float rs = 0.f;
@@ -154,7 +152,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
       float pv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        pv[i] = exp2f(s[t][i] - m_use);
+        pv[i] = __builtin_amdgcn_exp2f(fmaf(s[t][i], sc, -m_use));
         rs += pv[i];
       }
       if (DROPOUT) {
@@ -172,19 +170,38 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
         for (int j = 0; j < 4; ++j) pf[t][sp][j] = E::pack2(pv[8 * sp + 2 * j], pv[8 * sp + 2 * j + 1]);
     }
     l_run = l_run * alpha + rs;  // lane-partial row sum (the partner lane holds the rest)
-
-    // ---- O^T = alpha O^T + V^T P^T ---------------------------------------------------------
+    if (rescale) {
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+        for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp)
-          acc[dt] = E::mfma(lds_tr_frag<DT>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
-    }
+          acc[dt] = E::mfma(lds_tr_frag<DT, BN>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
+  };
 
+  for (int it = 0; it < ntiles; ++it) {
+    const int cur = it & 1;
+    const int n0 = it * BN;
+    if (it + 1 < ntiles) {  // prefetch the next K/V tile into the other buffer
+      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
+      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
+    }
+    // wave-uniform tile class: fully masked for this wave / needs masks / interior
+    const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
+    const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
+    if (!dead) {
+      if (need_mask)
+        tile(std::true_type{}, kt(cur), vt(cur), n0);
+      else
+        tile(std::false_type{}, kt(cur), vt(cur), n0);
+    }
     __builtin_amdgcn_s_waitcnt(0);  // next tile landed (LDS-DMA counts on vmcnt)
     __syncthreads();
   }
