@@ -14,8 +14,8 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 GEN = os.path.join(CSRC, "gen")
-OBJ = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libfa2_amd.so")
+OBJ = os.environ.get("FA2_BUILD_DIR", os.path.join(HERE, "_build"))
+LIB = os.environ.get("FA2_LIB_OUT", os.path.join(HERE, "libfa2_amd.so"))
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("FA2_OFFLOAD_ARCH", "gfx950")
 

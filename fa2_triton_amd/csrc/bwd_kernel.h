@@ -80,8 +80,10 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
-  const int n0 = blockIdx.x * BNK;
-  const int bkv = blockIdx.y;
+  const int nkb = (p.seqlen_k + BNK - 1) / BNK;
+  const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
+  const int bkv = item / nkb;
+  const int n0 = (item - bkv * nkb) * BNK;           // causal: low keys see the most rows
   const int b = bkv / p.heads_kv, hkv = bkv - b * p.heads_kv;
   const int G = p.heads_q / p.heads_kv;
   int Lq = p.seqlen_q, Lk = p.seqlen_k;
@@ -105,18 +107,28 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
   const int total = n_mt * G;  // (q-head, tile) steps
 
+  Stager<DT, BMQ, NT> qst, ost;
+  if (ALIGNED) {
+    qst.init(tid, p.q_stride[1], D);
+    ost.init(tid, p.do_stride[1], D);
+  }
   auto stage = [&](int step, int buf) {
     const int g = step / n_mt, mt = step - g * n_mt;
     const int hq = hkv * G + g;
     const int m = m_begin + mt * BMQ;
     const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
-    stage_tile<DT, BMQ, NT, ALIGNED>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
-    stage_tile<DT, BMQ, NT, ALIGNED>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
+    if constexpr (ALIGNED) {
+      qst.issue(qt(buf), qg, p.q_stride[1], m, Lq, tid);
+      ost.issue(ot(buf), og, p.do_stride[1], m, Lq, tid);
+    } else {
+      stage_tile<DT, BMQ, NT, false>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
+      stage_tile<DT, BMQ, NT, false>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
+    }
     if (w == 0) {  // LSE2 rows -> lanes 0..31, delta rows -> lanes 32..63 (one 256-byte piece)
       const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m + r32;
       const float* src = hh ? p.delta + srow : p.lse + srow;
-      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)st(buf), 4, 0, 0);
+      glds4(src, __builtin_amdgcn_readfirstlane(lds_addr(st(buf))));
     }
   };
 
@@ -135,22 +147,34 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
 
-  // rows q of this lane's key that survive the masks: q_lo <= q < Lq (none if the key is padding)
-  const int q_lo = CAUSAL ? max(kj - diag, 0) : 0;
-  const int q_hi = kval ? Lq : -1;
 
+  // Phases (sched_barrier-separated so each phase's LDS fragments stay inside it and the
+  // register peak stays under 256): S, dP -> P, dS -> dV, dK.
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BMQ>(Q, 0, r32, 2 * ks + hh), kf[ks], s);
-    __builtin_amdgcn_sched_barrier(0);  // keep each phase's fragment loads inside the phase
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      dp = E::mfma(lds_row_frag<DT, BMQ>(O, 0, r32, 2 * ks + hh), lds_row_frag<DT, BNK>(Vs, 32 * w, r32, 2 * ks + hh), dp);
+    for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BMQ>(Q, 0, r32, ks, hh), kf[ks], s);
     __builtin_amdgcn_sched_barrier(0);
-    // rows of register i: m + (i & 3) + 8 (i >> 2) + 4 hh
-    const int lo = q_lo - m - 4 * hh, hi = q_hi - m - 4 * hh;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      dp = E::mfma(lds_row_frag<DT, BMQ>(O, 0, r32, ks, hh), lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks, hh), dp);
+      if (ks & 1) __builtin_amdgcn_sched_barrier(0);  // at most two fragment pairs in flight
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // rows of register i: m + (i & 3) + 8 (i >> 2) + 4 hh.  The row window [q_lo, q_hi) of this
+    // lane's key is recomputed from an opaque lane id: hoisted out of the loop it gets spilled
+    // and its scratch reload would drain the LDS-DMA prefetch (vmcnt(0)).
+    int lo = 0, hi = 0;
+    if (MASK) {
+      int ln = threadIdx.x;
+      asm volatile("" : "+v"(ln));
+      const int kl = n0 + 32 * (ln >> 6) + (ln & 31);
+      const int qlo = CAUSAL ? max(kl - diag, 0) : 0;
+      const int qhi = kl < Lk ? Lq : -1;
+      lo = qlo - m - 4 * hh;
+      hi = qhi - m - 4 * hh;
+    }
     u32x4 pp[2], dsp[2];
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -187,11 +211,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         dv[dt] = E::mfma(lds_tr_frag<DT, BMQ>(O, 16 * sp, 32 * dt, lane), pp[sp], dv[dt]);
         dk[dt] = E::mfma(lds_tr_frag<DT, BMQ>(Q, 16 * sp, 32 * dt, lane), dsp[sp], dk[dt]);
       }
-      if (dt & 1) __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
+      __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
     }
   };
 
-  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
   __syncthreads();
   if (ALIGNED && D < DT && total > 0) {
     // dP = dO V^T reads both operands from LDS, whose clamped staging repeats the last real
@@ -220,7 +244,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       else
         body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    vm_wait_all();
     __syncthreads();
   }
 
@@ -258,15 +282,22 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 }
 
 // ---------------------------------------------------------------------------------------------
+template <int DT>
+struct DqCfg {
+  static constexpr int NW = DT >= 256 ? 4 : 8;
+  static constexpr int kWavesPerSimd = DT >= 256 ? 1 : 2;
+};
+
 // dQ: one workgroup = 4 waves = 128 query rows of one (batch, q-head); K/V tiles of 64 keys in
 // LDS (double buffered).  Per tile and wave:
 //   S^T, dP^T [key][q]   2 x (8 + 8) MFMA (A = K / V row fragments, B = Q / dO in VGPRs)
 //   dQ^T[d][q] += K^T dS^T   NDT*4 MFMA (A = K^T via ds_read_b64_tr_b16)
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED, bool DQF32>
-__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) dq_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NT = 256;
-  constexpr int BM = 128, BN = 64;
+  constexpr int NW = DqCfg<DT>::NW;
+  constexpr int NT = NW * 64;
+  constexpr int BM = NW * 32, BN = 64;
   constexpr int KS = DT / 16;
   constexpr int NDT = DT / 32;
   constexpr int TILE = BN * DT * 2;
@@ -274,9 +305,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
-  const int nmb = gridDim.x;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nmb = (p.seqlen_q + BM - 1) / BM;
+  const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
+  const int bh = item / nmb;
+  const int mbi = item - bh * nmb;
+  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;  // heaviest blocks first
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
   int Lq = p.seqlen_q, Lk = p.seqlen_k;
@@ -299,10 +332,21 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
   const int ntiles = (n_end + BN - 1) / BN;
   auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
   auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
-  if (ntiles > 0) {
-    stage_tile<DT, BN, NT, ALIGNED>(kt(0), kg, p.k_stride[1], 0, Lk, D, tid);
-    stage_tile<DT, BN, NT, ALIGNED>(vt(0), vg, p.v_stride[1], 0, Lk, D, tid);
+  Stager<DT, BN, NT> kst, vst;
+  if (ALIGNED) {
+    kst.init(tid, p.k_stride[1], D);
+    vst.init(tid, p.v_stride[1], D);
   }
+  auto stage_kv = [&](int buf, int n) {
+    if constexpr (ALIGNED) {
+      kst.issue(kt(buf), kg, p.k_stride[1], n, Lk, tid);
+      vst.issue(vt(buf), vg, p.v_stride[1], n, Lk, tid);
+    } else {
+      stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, Lk, D, tid);
+      stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, Lk, D, tid);
+    }
+  };
+  if (ntiles > 0) stage_kv(0, 0);
 
   const bool qvalid = qi < Lq;
   u32x4 qf[KS], of[KS];
@@ -323,7 +367,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
 
-  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
   __syncthreads();
 
   // key kj visible to this lane's row iff kj < lim_lane (0 for padded rows)
@@ -341,10 +385,10 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
       if (MASK && !(n0 + 32 * t < Lk && (!CAUSAL || n0 + 32 * t <= mw0 + 31 + diag))) continue;
       f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, 2 * ks + hh), qf[ks], s);
+      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, 2 * ks + hh), of[ks], dp);
+      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
       __builtin_amdgcn_sched_barrier(0);
       u32x4 dsp[2];
 #pragma unroll
@@ -383,10 +427,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
   for (int it = 0; it < ntiles; ++it) {
     const int cur = it & 1;
     const int n0 = it * BN;
-    if (it + 1 < ntiles) {
-      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
-      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
-    }
+    if (it + 1 < ntiles) stage_kv(cur ^ 1, n0 + BN);
     const bool dead = CAUSAL && (n0 > mw0 + 31 + diag);
     const bool need_mask = (n0 + BN > Lk) || (mw0 + 31 >= Lq) || (CAUSAL && n0 + BN - 1 > mw0 + diag);
     if (!dead) {
@@ -395,7 +436,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dq_kernel(const fa2_bw
       else
         tile(std::false_type{}, kt(cur), vt(cur), n0);
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    vm_wait_all();
     __syncthreads();
   }
 
@@ -442,15 +483,16 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, hipStream_t st) {
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   {
-    dim3 grid((a.seqlen_k + 127) / 128, a.batch * a.heads_kv);
+    dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
     hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   {
-    dim3 grid((a.seqlen_q + 127) / 128, a.batch * a.heads_q);
+    constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
+    dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, true>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
     else
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, false>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
   return hipGetLastError();
 }

@@ -99,6 +99,20 @@ FA2_DEV f32x16 zero16() {
 }
 
 // ---------------------------------------------------------------------------------------------
+// XCD-aware work order.  Workgroups are dealt round-robin to the 8 XCDs (block L -> XCD L % 8),
+// each with its own L2.  With a 2-D grid whose x extent is a multiple of 8, every XCD would get
+// the same few x indices for all heads -- under a causal mask that is 2.4x more work on one
+// XCD than on another.  Instead the work items are numbered head-major (all blocks of a head
+// consecutive, heaviest first) and XCD x gets one contiguous slice of that list (bijective
+// remap for any count): balanced work per XCD, and the blocks of a head -- which share its K/V
+// -- run together on one XCD's L2.
+FA2_DEV int xcd_item(int L, int total) {
+  const int x = L & 7, idx = L >> 3;
+  const int q = total >> 3, r = total & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + idx;
+}
+
+// ---------------------------------------------------------------------------------------------
 // LDS tile layout ("d-tile major").  A tile of ROWS x DT 16-bit elements is stored as DT/32
 // sub-tiles of ROWS x 32 columns; each sub-tile row is 64 bytes (four 16-byte chunks) and
 // chunk cc of row r sits at cc ^ ((r >> 2) & 3).  With this image
@@ -117,11 +131,13 @@ struct Tile {
   FA2_DEV static int off(int r, int c) { return (c >> 2) * kSub + r * 64 + (((c & 3) ^ ((r >> 2) & 3)) << 4); }
 };
 
-// 16-byte row fragment: row row0 + r32 (row0 % 16 == 0), chunk c  (A or B operand of a
-// 32x32x16 MFMA: element j = column 8c + j).
+// 16-byte row fragment for k-step ks of a 32x32x16 MFMA: row row0 + r32 (row0 % 16 == 0),
+// columns 16 ks + 8 hh + (0..7).  Written so that every (row0, ks) differs from the lane's
+// base address by an immediate (only the parity of ks changes the swizzled chunk).
 template <int DT, int ROWS>
-FA2_DEV u32x4 lds_row_frag(const char* tile, int row0, int r32, int c) {
-  const int off = (c >> 2) * Tile<DT, ROWS>::kSub + (row0 + r32) * 64 + (((c & 3) ^ ((r32 >> 2) & 3)) << 4);
+FA2_DEV u32x4 lds_row_frag(const char* tile, int row0, int r32, int ks, int hh) {
+  const int cc = ((ks & 1) << 1) | hh;
+  const int off = (ks >> 1) * Tile<DT, ROWS>::kSub + (row0 + r32) * 64 + ((cc ^ ((r32 >> 2) & 3)) << 4);
   return *(const u32x4*)(tile + off);
 }
 
@@ -145,6 +161,34 @@ FA2_DEV u32x4 lds_tr_frag(const char* tile, int row0, int col0, int lane) {
   u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
   return u32x4{a[0], a[1], b[0], b[1]};
 }
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA issued from inline asm.  hipcc tracks its own global_load_lds builtins and, unable to
+// tell the DMA's LDS destination from the buffer being read, inserts s_waitcnt vmcnt(0) before
+// the next ds_read -- which drains the next tile's prefetch in the middle of the current tile.
+// Issued from asm the DMA is invisible to that pass; the kernels retire it themselves with
+// vm_wait_all() right before the barrier that publishes the tile (the compiler's own waits
+// for its own loads only over-wait, never under-wait, since VMEM ops retire in issue order).
+FA2_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+FA2_DEV void glds16(const void* gsrc, uint32_t lds_base_uniform) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base_uniform)
+      : "memory");
+}
+FA2_DEV void glds4(const void* gsrc, uint32_t lds_base_uniform) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base_uniform)
+      : "memory");
+}
+FA2_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
 // Global -> LDS tile staging.  ROWS rows starting at global row `row0` (row stride
@@ -178,9 +222,7 @@ FA2_DEV void stage_tile(char* tile, const uint16_t* g, int64_t row_stride, int r
       grow = grow < row_end ? grow : row_end - 1;
       const int gc = c < dchunks ? c : dchunks - 1;
       const uint16_t* src = g + (int64_t)grow * row_stride + gc * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(tile + wbase * 16),
-                                       16, 0, 0);
+      glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(tile + wbase * 16)));
     }
   } else {
     // one thread per (row, chunk); 8 scalar loads each
@@ -200,6 +242,51 @@ FA2_DEV void stage_tile(char* tile, const uint16_t* g, int64_t row_stride, int r
     }
   }
 }
+
+// LDS-DMA stager for a ROWS x DT tile with the per-lane source offsets precomputed once
+// (row * row_stride + chunk * 8, elements), so that issuing a full tile costs one 64-bit add
+// per 16-byte piece.  Only a tile that crosses row_end takes the clamping path.
+template <int DT, int ROWS, int NTHREADS>
+struct Stager {
+  static constexpr int kPieces = ROWS * DT / 8;
+  static constexpr int kIters = (kPieces + NTHREADS - 1) / NTHREADS;
+  static_assert(kPieces % 64 == 0, "tile must be a whole number of wave pieces");
+  int32_t off[kIters];  // element offset of this lane's piece relative to the tile's first row
+  int wave;
+
+  FA2_DEV void init(int tid, int64_t row_stride, int D) {
+    wave = tid >> 6;
+    const int lane = tid & 63, dchunks = D >> 3;
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int piece = (it * (NTHREADS / 64) + wave) * 64 + lane;
+      const int sub = piece / (ROWS * 4), within = piece % (ROWS * 4);
+      const int pr = within >> 2;
+      const int c = sub * 4 + ((within & 3) ^ ((pr >> 2) & 3));
+      const int gc = c < dchunks ? c : dchunks - 1;
+      off[it] = (int32_t)(pr * row_stride) + gc * 8;
+    }
+  }
+  // rows [row0, row0 + ROWS) of g (row stride row_stride); rows >= row_end re-read row_end - 1
+  FA2_DEV void issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int tid) {
+    const uint16_t* gt = g + (int64_t)row0 * row_stride;
+    const bool full = row0 + ROWS <= row_end;
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int wbase = (it * (NTHREADS / 64) + wave) * 64;
+      if (kPieces % NTHREADS != 0 && wbase >= kPieces) break;  // wave-uniform
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(tile + wbase * 16));
+      if (full) {
+        glds16(gt + off[it], dst);
+      } else {
+        const int piece = wbase + (tid & 63);
+        const int pr = (piece % (ROWS * 4)) >> 2;
+        const int clamp = row0 + pr < row_end ? 0 : (row0 + pr - (row_end - 1));
+        glds16(gt + off[it] - (int64_t)clamp * row_stride, dst);
+      }
+    }
+  }
+};
 
 // 16-byte register fragment straight from global memory: elements [d0, d0 + 8) of one row;
 // zero outside [0, D) or when !valid.

@@ -12,6 +12,13 @@
 //   S^T[key][q] = K Q^T        16 MFMA 32x32x16 (A = K row frags from LDS, B = Q frags in VGPRs)
 //   softmax on the lane pair (l, l^32) holding one query row (16+16 keys per 32-key tile)
 //   O^T[d][q]  += V^T P^T      16 MFMA (A = V^T via ds_read_b64_tr_b16, B = P in registers)
+//
+// Ping-pong schedule (NW = 8): waves w and w+4 share a SIMD.  Each tile takes two barrier-
+// separated phases; in phase A waves 0-3 run QK^T + softmax of tile i while waves 4-7 run the
+// PV of tile i-1, in phase B the roles swap.  So on every SIMD one wave's softmax VALU and
+// fragment reads overlap its partner's MFMAs, instead of both waves hitting LDS, MFMA and VALU
+// in lockstep.  K_{i+1} is issued at the start of A_i and V_{i+1} at the start of B_i (each
+// two phases ahead of its first reader), retired by counted vmcnt waits before the barriers.
 #include <type_traits>
 
 #include "common.h"
@@ -19,25 +26,42 @@
 
 namespace fa2 {
 
+// Waves per workgroup: 8 (256 query rows share each K/V tile, one workgroup per CU, two waves
+// per SIMD) up to DT = 128; 4 for DT = 256, whose ~300 live registers allow one wave per SIMD.
+template <int DT>
+struct FwdCfg {
+  static constexpr int NW = DT >= 256 ? 4 : 8;
+  static constexpr int kWavesPerSimd = DT >= 256 ? 1 : 2;
+};
+
+// Defer-max threshold (log2 units): the running row max is only moved -- and O rescaled --
+// when some row of the wave grows by more than this; P then stays <= 2^kDeferMax, which fp32
+// accumulation and bf16/fp16 P (same relative precision at any magnitude) absorb exactly.
+constexpr float kDeferMax = 8.f;
+
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
-__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_fwd_args p) {
+__global__ void __launch_bounds__(FwdCfg<DT>::NW * 64, FwdCfg<DT>::kWavesPerSimd) fwd_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = 4;
+  constexpr int NW = FwdCfg<DT>::NW;
+  constexpr bool PINGPONG = NW == 8;
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
   constexpr int KS = DT / 16;        // k-steps of Q K^T
   constexpr int NDT = DT / 32;       // 32-wide d tiles of O
   constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
+  const int grp = PINGPONG ? (w >> 2) : 0;  // phase offset of this wave
 
   // ---- work item -----------------------------------------------------------------------
-  const int nmb = gridDim.x;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heavy rows first
-  const int bh = blockIdx.y;
+  const int nmb = (p.seqlen_q + BM - 1) / BM;
+  const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
+  const int bh = item / nmb;
+  const int mbi = item - bh * nmb;
+  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;  // heaviest (longest key range) blocks first
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
   int Lq = p.seqlen_q, Lk = p.seqlen_k, cu = 0;
@@ -62,12 +86,24 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
   }
   const int ntiles = (n_end + BN - 1) / BN;
 
-  // stage tile 0 first so its latency overlaps the Q fragment loads
-  auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
-  auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
+  auto kt = [&](int buf) { return smem + buf * TILE; };
+  auto vt = [&](int buf) { return smem + (2 + buf) * TILE; };
+  Stager<DT, BN, NT> kst, vst;
+  if (ALIGNED) {
+    kst.init(tid, p.k_stride[1], D);
+    vst.init(tid, p.v_stride[1], D);
+  }
+  auto stage_k = [&](int buf, int n0) {
+    if constexpr (ALIGNED) kst.issue(kt(buf), kg, p.k_stride[1], n0, Lk, tid);
+    else stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n0, Lk, D, tid);
+  };
+  auto stage_v = [&](int buf, int n0) {
+    if constexpr (ALIGNED) vst.issue(vt(buf), vg, p.v_stride[1], n0, Lk, tid);
+    else stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n0, Lk, D, tid);
+  };
   if (ntiles > 0) {
-    stage_tile<DT, BN, NT, ALIGNED>(kt(0), kg, p.k_stride[1], 0, Lk, D, tid);
-    stage_tile<DT, BN, NT, ALIGNED>(vt(0), vg, p.v_stride[1], 0, Lk, D, tid);
+    stage_k(0, 0);
+    stage_v(0, 0);
   }
 
   // ---- Q fragments (B operand of S^T = K Q^T): Q[qi][16 ks + 8 hh + j] -------------------
@@ -87,16 +123,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
   for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
 
   const char* biasb = nullptr;
-  if (BIAS)
-    biasb = (const char*)p.bias;
+  if (BIAS) biasb = (const char*)p.bias;
   uint64_t drop_base = 0;
   if (DROPOUT) {
     // flat Philox offset, /root/reference/src/forward/kernel.py:146-148 (int64 here)
     drop_base = (uint64_t)Lk * ((uint64_t)cu + (uint64_t)Lq * ((uint64_t)hq + (uint64_t)p.heads_q * (p.cu_seqlens ? 0 : b)));
   }
-
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
 
   // Per-lane key limit: key kj is visible to this lane's row iff kj < lim_lane.
   const int qw0 = m0 + w * 32;  // first row of this wave
@@ -104,17 +136,20 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
   // Scores are kept raw (no bias) or already in base-2 units (bias): exp2 argument = x*sc - m.
   const float sc = BIAS ? 1.f : scale2;
 
-  // One 64-key tile for this wave.  MASK selects the diagonal / tail variant at compile time so
-  // the common interior tile carries no per-element compare.
-  auto tile = [&](auto mask_c, const char* K, const char* V, int n0) {
+  // state handed from a wave's QK phase to its PV phase
+  u32x4 pf[2][2];
+  float alpha = 1.f;
+  bool rescale = false;
+
+  // QK^T + online softmax of one 64-key tile for this wave (MASK: diagonal / tail variant).
+  auto qk_softmax = [&](auto mask_c, const char* K, int n0) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       s[t] = zero16();
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        s[t] = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, 2 * ks + hh), qf[ks], s[t]);
+      for (int ks = 0; ks < KS; ++ks) s[t] = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s[t]);
     }
     // register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
     const int rel = lim_lane - n0 - 4 * hh;
@@ -138,15 +173,15 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
       }
     }
     mx = half_max(mx) * sc;
-    const float m_new = fmaxf(m_run, mx);
+    // defer-max: keep the stale max unless some row of the wave outgrew it by > kDeferMax
+    // (the first finite max always moves it: -inf - m is never <= threshold)
+    rescale = !__all(mx - m_run <= kDeferMax);
+    const float m_new = rescale ? fmaxf(m_run, mx) : m_run;
     const float m_use = m_new == kNegInf ? 0.f : m_new;
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
-    // exact lazy rescale: skip the O pass when no row max of the wave moved
-    const bool rescale = !__all(m_new == m_run);
+    alpha = __builtin_amdgcn_exp2f(m_run - m_use);
     m_run = m_new;
 
     float rs = 0.f;
-    u32x4 pf[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       float pv[16];
@@ -170,13 +205,16 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
         for (int j = 0; j < 4; ++j) pf[t][sp][j] = E::pack2(pv[8 * sp + 2 * j], pv[8 * sp + 2 * j + 1]);
     }
     l_run = l_run * alpha + rs;  // lane-partial row sum (the partner lane holds the rest)
+  };
+
+  // O^T = alpha O^T + V^T P^T
+  auto pv_update = [&](const char* V) {
     if (rescale) {
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
     }
-    // O^T += V^T P^T
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -186,23 +224,50 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
           acc[dt] = E::mfma(lds_tr_frag<DT, BN>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
   };
 
-  for (int it = 0; it < ntiles; ++it) {
-    const int cur = it & 1;
-    const int n0 = it * BN;
-    if (it + 1 < ntiles) {  // prefetch the next K/V tile into the other buffer
-      stage_tile<DT, BN, NT, ALIGNED>(kt(cur ^ 1), kg, p.k_stride[1], n0 + BN, Lk, D, tid);
-      stage_tile<DT, BN, NT, ALIGNED>(vt(cur ^ 1), vg, p.v_stride[1], n0 + BN, Lk, D, tid);
+  __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
+  __syncthreads();
+
+  // Phase ph = 2 i + x: x = 0 (A_i) issues K_{i+1}, x = 1 (B_i) issues V_{i+1}.  A wave of
+  // group g runs QK of tile (ph - g) / 2 when ph - g is even, PV of tile (ph - g - 1) / 2 when odd.
+  constexpr int kPieces = Stager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
+  const int nphase = ntiles > 0 ? 2 * ntiles + (PINGPONG ? 1 : 0) : 0;
+  bool live = false;  // the pending PV of this wave has unmasked rows
+  for (int ph = 0; ph < nphase; ++ph) {
+    const int i = ph >> 1;
+    const bool issued = ((ph & 1) == 0) ? (i + 1 < ntiles) : (i + 1 < ntiles);
+    if (i + 1 < ntiles) {
+      if ((ph & 1) == 0) stage_k((i + 1) & 1, (i + 1) * BN);
+      else stage_v((i + 1) & 1, (i + 1) * BN);
     }
-    // wave-uniform tile class: fully masked for this wave / needs masks / interior
-    const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
-    const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
-    if (!dead) {
-      if (need_mask)
-        tile(std::true_type{}, kt(cur), vt(cur), n0);
-      else
-        tile(std::false_type{}, kt(cur), vt(cur), n0);
+    const int rel_ph = ph - grp;
+    if (rel_ph >= 0) {
+      const int tile = rel_ph >> 1;
+      if ((rel_ph & 1) == 0) {
+        if (tile < ntiles) {
+          const int n0 = tile * BN;
+          // wave-uniform tile class: fully masked for this wave / needs masks / interior
+          const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
+          const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
+          live = !dead;
+          if (!dead) {
+            if (need_mask) qk_softmax(std::true_type{}, kt(tile & 1), n0);
+            else qk_softmax(std::false_type{}, kt(tile & 1), n0);
+          }
+        }
+      } else if (live) {
+        pv_update(vt(tile & 1));
+        live = false;
+      }
     }
-    __builtin_amdgcn_s_waitcnt(0);  // next tile landed (LDS-DMA counts on vmcnt)
+    // retire the tile the next phase reads; the DMA issued in this phase may stay in flight
+    if (PINGPONG && issued) {
+      if constexpr (kPieces == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if constexpr (kPieces == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (kPieces == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else vm_wait_all();
+    } else {
+      vm_wait_all();
+    }
     __syncthreads();
   }
 
@@ -240,9 +305,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) fwd_kernel(const fa2_f
 // ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int BM = 128;
-  dim3 grid((a.seqlen_q + BM - 1) / BM, a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
+  constexpr int NW = FwdCfg<DT>::NW, BM = NW * 32;
+  dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+  hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
 
