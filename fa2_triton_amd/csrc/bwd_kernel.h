@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 // ---------------------------------------------------------------------------------------------
 template <int DT>
 struct DqCfg {
-  static constexpr int NW = DT >= 256 ? 4 : 8;
+  static constexpr int NW = 4;  // two independent workgroups per CU (measured faster than 8 waves)
   static constexpr int kWavesPerSimd = DT >= 256 ? 1 : 2;
 };
 

@@ -28,9 +28,12 @@ namespace fa2 {
 
 // Waves per workgroup: 8 (256 query rows share each K/V tile, one workgroup per CU, two waves
 // per SIMD) up to DT = 128; 4 for DT = 256, whose ~300 live registers allow one wave per SIMD.
-template <int DT>
+// Causal: 4 waves (two independent workgroups per CU desynchronise each SIMD's pair of waves
+// by themselves, and 128-row blocks waste less on the diagonal); non-causal: 8 waves with the
+// ping-pong schedule below.
+template <int DT, bool CAUSAL>
 struct FwdCfg {
-  static constexpr int NW = DT >= 256 ? 4 : 8;
+  static constexpr int NW = (DT >= 256 || CAUSAL) ? 4 : 8;
   static constexpr int kWavesPerSimd = DT >= 256 ? 1 : 2;
 };
 
@@ -40,9 +43,9 @@ struct FwdCfg {
 constexpr float kDeferMax = 8.f;
 
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
-__global__ void __launch_bounds__(FwdCfg<DT>::NW * 64, FwdCfg<DT>::kWavesPerSimd) fwd_kernel(const fa2_fwd_args p) {
+__global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAUSAL>::kWavesPerSimd)) fwd_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = FwdCfg<DT>::NW;
+  constexpr int NW = FwdCfg<DT, CAUSAL>::NW;
   constexpr bool PINGPONG = NW == 8;
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
@@ -230,8 +233,27 @@ __global__ void __launch_bounds__(FwdCfg<DT>::NW * 64, FwdCfg<DT>::kWavesPerSimd
   // Phase ph = 2 i + x: x = 0 (A_i) issues K_{i+1}, x = 1 (B_i) issues V_{i+1}.  A wave of
   // group g runs QK of tile (ph - g) / 2 when ph - g is even, PV of tile (ph - g - 1) / 2 when odd.
   constexpr int kPieces = Stager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
-  const int nphase = ntiles > 0 ? 2 * ntiles + (PINGPONG ? 1 : 0) : 0;
   bool live = false;  // the pending PV of this wave has unmasked rows
+  if constexpr (!PINGPONG) {
+    // one barrier per tile: prefetch K/V_{i+1}, QK + softmax + PV of tile i
+    for (int i = 0; i < ntiles; ++i) {
+      if (i + 1 < ntiles) {
+        stage_k((i + 1) & 1, (i + 1) * BN);
+        stage_v((i + 1) & 1, (i + 1) * BN);
+      }
+      const int n0 = i * BN;
+      const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
+      const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
+      if (!dead) {
+        if (need_mask) qk_softmax(std::true_type{}, kt(i & 1), n0);
+        else qk_softmax(std::false_type{}, kt(i & 1), n0);
+        pv_update(vt(i & 1));
+      }
+      vm_wait_all();
+      __syncthreads();
+    }
+  }
+  const int nphase = PINGPONG && ntiles > 0 ? 2 * ntiles + 1 : 0;
   for (int ph = 0; ph < nphase; ++ph) {
     const int i = ph >> 1;
     const bool issued = ((ph & 1) == 0) ? (i + 1 < ntiles) : (i + 1 < ntiles);
@@ -305,7 +327,7 @@ __global__ void __launch_bounds__(FwdCfg<DT>::NW * 64, FwdCfg<DT>::kWavesPerSimd
 // ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int NW = FwdCfg<DT>::NW, BM = NW * 32;
+  constexpr int NW = FwdCfg<DT, CAUSAL>::NW, BM = NW * 32;
   dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
   hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
