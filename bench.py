@@ -8,10 +8,12 @@ one forward + one backward of that batch.  With N GPUs each rank runs its own B=
 
 FLOPs are algorithmic: fwd = 4 B H S^2 D / 2 (causal), bwd = 2.5 fwd.
 
-Besides the step time, the forward kernel (the north-star kernel) and the backward launch
-(delta + dK/dV + dQ kernels) are timed with HIP events on the stream they run on, giving the
-`roofline` object, and rank 0 times the CPU oracle (oracle/reference.py, fp32, torch CPU
-threads) on a bounded slice of the same workload for `cpu_baseline`.
+Besides the step time, every launch of the path -- forward, and the backward's delta, dK/dV and
+dQ kernels (fa2_bwd_stages) -- is timed with HIP events on the stream it runs on.  `roofline`
+is the dominant (longest) kernel, `roofline_fwd` the north-star forward kernel, each with its
+algorithmic FLOPs per launch and the HBM bytes per launch from the committed rocprofv3 PMC
+summary (profiles/*_pmc.json).  Rank 0 also times the CPU oracle (oracle/reference.py, fp32,
+torch CPU threads) on a bounded slice of the same workload for `cpu_baseline`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -32,6 +34,18 @@ METRIC = "attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16; % of MFMA peak
 def attn_flops(b, h, sq, sk, d, causal):
     f = 4.0 * b * h * sq * sk * d
     return f * 0.5 if causal else f
+
+
+def load_pmc():
+    """HBM bytes per launch from the latest committed rocprofv3 PMC summary (profiles/*_pmc.json,
+    FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), valid for the default workload only."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc.json")))
+    if not files:
+        return {}
+    data = json.load(open(files[-1]))
+    return {k.replace("fa2::", ""): v for k, v in data.items()}
 
 
 def cpu_baseline(b, h, s, d, causal, budget_s=20.0):
@@ -59,13 +73,21 @@ def cpu_baseline(b, h, s, d, causal, budget_s=20.0):
             break
         heads //= 2
     heads, dt = best
+    reps = 1
+    while dt * reps < 10.0 and reps < 8:  # about 10 s of CPU work in total
+        t0 = time.perf_counter()
+        out = attention_reference(q, k, v, causal=causal)
+        torch.autograd.grad(out, (q, k, v), do)
+        dt = (dt * reps + time.perf_counter() - t0) / (reps + 1)
+        reps += 1
     flops = 3.5 * attn_flops(1, heads, s, s, d, causal)
     return {
         "value": flops / dt / 1e12,
         "unit": "TFLOP/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"oracle fp32 fwd+bwd, B=1 H={heads} S={s} D={d} causal={causal} (slice of the workload), {dt:.2f} s",
+        "sample": f"oracle fp32 fwd+bwd, B=1 H={heads} S={s} D={d} causal={causal} (slice of the workload), "
+                  f"mean of {reps} reps, {dt:.2f} s each",
     }
 
 
@@ -135,23 +157,64 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- per-launch timing with HIP events on the launch stream ---------------------------
+    # fwd: one launch; bwd: delta, dK/dV and dQ launches timed separately via fa2_bwd_stages.
     reps = max(5, args.steps)
     stream = torch.cuda.current_stream(device)
     with torch.no_grad():
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        ev[0].record(stream)
-        for _ in range(reps):
-            _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
-        ev[1].record(stream)
-        for _ in range(reps):
-            _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None)
-        ev[2].record(stream)
-        torch.cuda.synchronize()
-    t_fwd = ev[0].elapsed_time(ev[1]) / reps * 1e-3
-    t_bwd = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+        calls = {
+            "fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
+            "delta_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
+                                                         _stages=1),
+            "dkdv_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
+                                                        _stages=2),
+            "dq_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
+                                                      _stages=4),
+        }
+        times = {}
+        for name, fn in calls.items():
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[name] = e0.elapsed_time(e1) / reps * 1e-3
+    t_fwd = times["fwd_kernel"]
+    t_bwd = times["delta_kernel"] + times["dkdv_kernel"] + times["dq_kernel"]
     fwd_tf = f_fwd / t_fwd / 1e12
     bwd_tf = 2.5 * f_fwd / t_bwd / 1e12
+    # Algorithmic FLOPs per launch: fwd = F; the backward's 5 GEMM-units
+    # (2.5 F) are split as S, dP, dV, dK -> dK/dV kernel (2 F) and dQ -> dQ kernel (0.5 F).
+    # The dQ kernel also recomputes S and dP (1 F executed but not algorithmic).
+    algo = {"fwd_kernel": f_fwd, "delta_kernel": 0.0, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd}
+    executed = {"fwd_kernel": f_fwd, "delta_kernel": 0.0, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 1.5 * f_fwd}
+    kernels = {
+        name: {
+            "ms": round(t * 1e3, 4),
+            "algorithmic_tflops": round(algo[name] / t / 1e12, 1),
+            "executed_mfma_tflops": round(executed[name] / t / 1e12, 1),
+        }
+        for name, t in times.items()
+    }
+    pmc = load_pmc()
+    pmc["_workload_ok"] = (b, h, s, d, causal) == (8, 32, 4096, 128, True)
+    dominant = max(("fwd_kernel", "dkdv_kernel", "dq_kernel"), key=lambda n: times[n])
+
+    def roofline(name):
+        ach = algo[name] / times[name] / 1e12
+        traffic = pmc.get(name, {}).get("hbm_bytes_per_launch") if pmc.get("_workload_ok") else None
+        return {
+            "bound": "mfma",
+            "kernel": f"fa2::{name}",
+            "achieved": round(ach, 2),
+            "peak": PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "algorithmic_flop_per_launch": algo[name],
+        }
 
     if rank != 0:
         if dist:
@@ -189,23 +252,9 @@ def main():
         "bwd_ms": round(t_bwd * 1e3, 4),
         "pct_of_peak_fwd": round(100 * fwd_tf / PEAK_TFLOPS, 2),
         "pct_of_peak_fwd_bwd": round(100 * value / world / PEAK_TFLOPS, 2),
-        "roofline": {
-            "bound": "mfma",
-            "kernel": "fa2::fwd_kernel (forward, one launch per call)",
-            "achieved": round(fwd_tf, 2),
-            "peak": PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(fwd_tf / PEAK_TFLOPS, 4),
-            "traffic": None,
-        },
-        "roofline_bwd": {
-            "bound": "mfma",
-            "kernel": "delta + dkdv + dq launches of one fa2_bwd call",
-            "achieved": round(bwd_tf, 2),
-            "peak": PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(bwd_tf / PEAK_TFLOPS, 4),
-        },
+        "roofline": roofline(dominant),
+        "roofline_fwd": roofline("fwd_kernel"),
+        "kernels": kernels,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

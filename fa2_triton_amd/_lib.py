@@ -97,7 +97,8 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_cu_seqlens_from_mask", "fa2_last_error", "fa2_version")
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_cu_seqlens_from_mask", "fa2_last_error",
+                    "fa2_version")
 
 _lock = threading.Lock()
 _lib = None
@@ -121,6 +122,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_fwd.restype = ctypes.c_int
         lib.fa2_bwd.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_void_p]
         lib.fa2_bwd.restype = ctypes.c_int
+        lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.c_void_p]
+        lib.fa2_bwd_stages.restype = ctypes.c_int
         lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
         lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int

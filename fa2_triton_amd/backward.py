@@ -34,6 +34,7 @@ def _flash_attn_backward(
     softmax_scale: Optional[float],
     dropout_seed: Optional[int],
     dq_dtype: Optional[torch.dtype] = None,
+    _stages: int = 7,
 ) -> Tuple[Tensor, Tensor, Tensor]:
     if attention_mask is not None:
         assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
@@ -85,5 +86,5 @@ def _flash_attn_backward(
     args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
     lib = _lib.load()
     with torch.cuda.device(q.device):
-        _lib.check(lib.fa2_bwd(ctypes.byref(args), stream_of(q)))
+        _lib.check(lib.fa2_bwd_stages(ctypes.byref(args), _stages, stream_of(q)))
     return dq, dk, dv

@@ -37,10 +37,11 @@ def generated_sources():
         for dname, flag in DTYPES.items():
             for dt in TILES:
                 path = os.path.join(GEN, f"{kind}_{dname}_d{dt}.hip")
+                extra = ", int" if kind == "bwd" else ""
                 body = (
                     f'#include "../{kind}_kernel.h"\n'
                     f"namespace fa2 {{\n"
-                    f"template hipError_t launch_{kind}_dt<{flag}, {dt}>(const fa2_{kind}_args&, bool, hipStream_t);\n"
+                    f"template hipError_t launch_{kind}_dt<{flag}, {dt}>(const fa2_{kind}_args&, bool{extra}, hipStream_t);\n"
                     f"}}\n"
                 )
                 if not os.path.exists(path) or open(path).read() != body:

@@ -100,7 +100,7 @@ int fa2_fwd(const fa2_fwd_args* a, void* stream) {
   return hip_status(e, "fa2_fwd launch");
 }
 
-int fa2_bwd(const fa2_bwd_args* a, void* stream) {
+int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   if (!a) return fail(FA2_E_INVALID, "null args");
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
@@ -111,6 +111,7 @@ int fa2_bwd(const fa2_bwd_args* a, void* stream) {
   if (a->dq_dtype != a->dtype && a->dq_dtype != FA2_F32) return fail(FA2_E_INVALID, "dq dtype %d", a->dq_dtype);
   if (a->bias && a->bias_dtype != FA2_F16 && a->bias_dtype != FA2_BF16 && a->bias_dtype != FA2_F32)
     return fail(FA2_E_INVALID, "bias dtype %d", a->bias_dtype);
+  if (stages & ~7) return fail(FA2_E_INVALID, "stage mask %d", stages);
   if (a->seqlen_q == 0 && a->seqlen_k == 0) return FA2_OK;
   const int D = a->head_dim;
   bool aligned = vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
@@ -125,17 +126,19 @@ int fa2_bwd(const fa2_bwd_args* a, void* stream) {
   const int dt = pick_dt(D);
   hipError_t e;
   if (bf)
-    e = dispatch_dt(dt, [&] { return fa2::launch_bwd_dt<true, 32>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<true, 64>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<true, 128>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<true, 256>(*a, aligned, st); });
+    e = dispatch_dt(dt, [&] { return fa2::launch_bwd_dt<true, 32>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<true, 64>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<true, 128>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<true, 256>(*a, aligned, stages, st); });
   else
-    e = dispatch_dt(dt, [&] { return fa2::launch_bwd_dt<false, 32>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<false, 64>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<false, 128>(*a, aligned, st); },
-                    [&] { return fa2::launch_bwd_dt<false, 256>(*a, aligned, st); });
+    e = dispatch_dt(dt, [&] { return fa2::launch_bwd_dt<false, 32>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<false, 64>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<false, 128>(*a, aligned, stages, st); },
+                    [&] { return fa2::launch_bwd_dt<false, 256>(*a, aligned, stages, st); });
   return hip_status(e, "fa2_bwd launch");
 }
+
+int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, 7, stream); }
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,
                              int32_t* cu_seqlens, void* stream) {

@@ -477,16 +477,16 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 
 // ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
-static hipError_t launch_bwd_t(const fa2_bwd_args& a, hipStream_t st) {
-  {
+static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
+  if (stages & 1) {
     dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
   }
-  {
+  if (stages & 2) {
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
     hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED>), grid, dim3(256), 0, st, a);
   }
-  {
+  if (stages & 4) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
     dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
@@ -498,10 +498,10 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, hipStream_t st) {
 }
 
 template <bool BF16, int DT>
-hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, hipStream_t st) {
+hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStream_t st) {
   const bool c = a.causal != 0, bi = a.bias != nullptr;
 #define FA2_BWD_CASE(C, B, A) \
-  if (c == C && bi == B && aligned == A) return launch_bwd_t<BF16, DT, C, B, A>(a, st);
+  if (c == C && bi == B && aligned == A) return launch_bwd_t<BF16, DT, C, B, A>(a, stages, st);
   FA2_BWD_CASE(true, true, true)
   FA2_BWD_CASE(true, true, false)
   FA2_BWD_CASE(true, false, true)

@@ -109,6 +109,11 @@ typedef struct fa2_bwd_args {
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
 int fa2_bwd(const fa2_bwd_args* args, void* stream);
 
+/* fa2_bwd restricted to some of its three launches (bit 0: delta = rowsum(O * dO), bit 1:
+ * dK/dV, bit 2: dQ; each later stage needs the earlier ones' outputs) -- for per-kernel timing
+ * and profiling; fa2_bwd == fa2_bwd_stages(args, 7, stream). */
+int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
+
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,
  * row stride mask_row_stride bytes).  Replaces attention_mask.sum(1).cumsum(0) and the
  * .item() syncs of the reference callers (src/forward/caller.py:48-50, src/utils.py:8-17). */

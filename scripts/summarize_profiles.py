@@ -1,0 +1,45 @@
+"""Condense rocprofv3 outputs of scripts/profile_round.sh into profiles/<tag>_*.{csv,json}."""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = f"gpurun_out/prof_{tag}"
+dst = "profiles"
+os.makedirs(dst, exist_ok=True)
+stats = glob.glob(f"{src}/bench/**/*kernel_stats.csv", recursive=True)[0]
+shutil.copy(stats, f"{dst}/{tag}_bench_kernel_stats.csv")
+
+
+def counters(sub):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(f"{src}/{sub}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            if "fa2::" not in name:
+                continue
+            short = name.split("<")[0].replace("void ", "")
+            agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+
+
+fetch, write, sq = counters("fetch"), counters("write"), counters("sq")
+out = {}
+for k in sorted(set(fetch) | set(write) | set(sq)):
+    e = {}
+    if k in fetch:
+        # gfx950: FETCH_SIZE (KB) counts half the bytes of wide coalesced reads -> x2 (MI355X_MICROARCH.md, HBM)
+        e["fetch_bytes_raw"] = fetch[k]["FETCH_SIZE"] * 1024
+        e["fetch_bytes_corrected"] = 2 * e["fetch_bytes_raw"]
+    if k in write:
+        e["write_bytes"] = write[k]["WRITE_SIZE"] * 1024
+    if "fetch_bytes_corrected" in e and "write_bytes" in e:
+        e["hbm_bytes_per_launch"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+    e.update({c: v for c, v in sq.get(k, {}).items()})
+    out[k] = e
+json.dump(out, open(f"{dst}/{tag}_pmc.json", "w"), indent=1)
+print(json.dumps(out, indent=1))
