@@ -36,6 +36,26 @@ def attn_flops(b, h, sq, sk, d, causal):
     return f * 0.5 if causal else f
 
 
+def reduce_elapsed(elapsed: float, dist, device) -> float:
+    """Slowest rank's wall time: the job is done when every shard is (max over ranks)."""
+    if dist is None:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def job_throughput(f_fwd: float, steps: int, world: int, elapsed: float):
+    """Whole-job algorithmic TFLOP/s (fwd + bwd = 3.5 fwd per step per rank) and ms per step."""
+    return 3.5 * f_fwd * steps * world / elapsed / 1e12, elapsed / steps * 1e3
+
+
+def shard_batch(global_batch: int, world: int, rank: int):
+    """Batch rows [lo, hi) of this rank (configs[3]: B=64 over 8 GPUs -> 8 per rank)."""
+    per = global_batch // world
+    return rank * per, rank * per + per
+
+
 def load_pmc():
     """HBM bytes per launch from the latest committed rocprofv3 PMC summary (profiles/*_pmc.json,
     FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), valid for the default workload only."""
@@ -119,7 +139,9 @@ def main():
     from fa2_triton_amd.backward import _flash_attn_backward
     from fa2_triton_amd.forward import _flash_attn_forward
 
-    b, h, s, d = args.batch, args.heads, args.seqlen, args.head_dim
+    # weak scaling: the global batch is --batch per GPU; this rank owns rows [lo, hi) of it
+    lo, hi = shard_batch(args.batch * world, world, rank)
+    b, h, s, d = hi - lo, args.heads, args.seqlen, args.head_dim
     causal = not args.no_causal
     dtype = torch.bfloat16
     torch.manual_seed(1234 + rank)
@@ -144,17 +166,10 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = reduce_elapsed(time.perf_counter() - t0, dist, device)
 
     f_fwd = attn_flops(b, h, s, s, d, causal)
-    f_step = 3.5 * f_fwd
-    total = f_step * args.steps * world
-    value = total / elapsed / 1e12
-    ms_per_step = elapsed / args.steps * 1e3
+    value, ms_per_step = job_throughput(f_fwd, args.steps, world, elapsed)
 
     # ---- per-launch timing with HIP events on the launch stream ---------------------------
     # fwd: one launch; bwd: delta, dK/dV and dQ launches timed separately via fa2_bwd_stages.
