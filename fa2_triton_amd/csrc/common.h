@@ -253,9 +253,11 @@ struct Stager {
   static_assert(kPieces % 64 == 0, "tile must be a whole number of wave pieces");
   int32_t off[kIters];  // element offset of this lane's piece relative to the tile's first row
   int wave;
+  uint32_t wave_lds;    // byte offset of this wave's first piece (wave-uniform, SGPR)
 
   FA2_DEV void init(int tid, int64_t row_stride, int D) {
     wave = tid >> 6;
+    wave_lds = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
     const int lane = tid & 63, dchunks = D >> 3;
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
@@ -270,19 +272,22 @@ struct Stager {
   // rows [row0, row0 + ROWS) of g (row stride row_stride); rows >= row_end re-read row_end - 1
   FA2_DEV void issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int tid) {
     const uint16_t* gt = g + (int64_t)row0 * row_stride;
-    const bool full = row0 + ROWS <= row_end;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds;
+    if (row0 + ROWS <= row_end) {  // whole tile in range: one add per piece
 #pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-      const int wbase = (it * (NTHREADS / 64) + wave) * 64;
-      if (kPieces % NTHREADS != 0 && wbase >= kPieces) break;  // wave-uniform
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(tile + wbase * 16));
-      if (full) {
-        glds16(gt + off[it], dst);
-      } else {
+      for (int it = 0; it < kIters; ++it) {
+        if (kPieces % NTHREADS != 0 && (it * (NTHREADS / 64) + wave) * 64 >= kPieces) break;
+        glds16(gt + off[it], base + it * NTHREADS * 16);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) {
+        const int wbase = (it * (NTHREADS / 64) + wave) * 64;
+        if (kPieces % NTHREADS != 0 && wbase >= kPieces) break;  // wave-uniform
         const int piece = wbase + (tid & 63);
         const int pr = (piece % (ROWS * 4)) >> 2;
         const int clamp = row0 + pr < row_end ? 0 : (row0 + pr - (row_end - 1));
-        glds16(gt + off[it] - (int64_t)clamp * row_stride, dst);
+        glds16(gt + off[it] - (int64_t)clamp * row_stride, base + it * NTHREADS * 16);
       }
     }
   }
