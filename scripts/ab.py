@@ -1,0 +1,59 @@
+"""A/B timing of several libfa2_amd.so builds in ONE process (interleaved rounds), cfg3 causal.
+
+usage: python scripts/ab.py lib_a.so lib_b.so [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd)
+"""
+import ctypes
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import fa2_triton_amd._lib as L  # noqa: E402
+from fa2_triton_amd.backward import _flash_attn_backward  # noqa: E402
+from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
+
+libs = []
+for path in sys.argv[1:]:
+    lib = ctypes.CDLL(os.path.abspath(path))
+    lib.fa2_fwd.argtypes = [ctypes.POINTER(L.FwdArgs), ctypes.c_void_p]
+    lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(L.BwdArgs), ctypes.c_int, ctypes.c_void_p]
+    lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+    lib.fa2_last_error.restype = ctypes.c_char_p
+    libs.append((os.path.basename(path), lib))
+
+b, h, s, d = 8, 32, 4096, 128
+causal = os.environ.get("CAUSAL", "1") == "1"
+what = os.environ.get("WHAT", "fwd,dkdv,dq").split(",")
+torch.manual_seed(0)
+q = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
+k = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
+v = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
+do = torch.randn_like(q)
+F = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
+flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F}
+results = {(n, w): [] for n, _ in libs for w in what}
+for rnd in range(5):
+    for name, lib in libs:
+        L._lib = lib
+        o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        calls = {
+            "fwd": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
+            "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=3),
+            "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=5),
+        }
+        for w in what:
+            calls[w]()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                calls[w]()
+            e1.record()
+            torch.cuda.synchronize()
+            results[(name, w)].append(e0.elapsed_time(e1) / 5)
+for (name, w), ts in results.items():
+    ts = sorted(ts)
+    med = ts[len(ts) // 2]
+    print(f"{name:28s} {w:5s} median {med:.3f} ms  min {ts[0]:.3f}  {flops[w] / med / 1e9:.0f} TFLOP/s executed")
