@@ -63,7 +63,10 @@ def compile_one(src: str, force: bool, dep_t: float) -> str:
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(dep_t, os.path.getmtime(src)):
         return obj
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-           "-I", CSRC, "-I", INCLUDE, "-Wno-unused-result"]
+           "-I", CSRC, "-I", INCLUDE, "-Wno-unused-result",
+           # MFMA accumulators in arch VGPRs: at one wave per SIMD (fwd_w64_kernel.h) the
+           # default heuristic puts them in AGPRs and copies the O tile through VGPRs per tile
+           "-mllvm", "-amdgpu-mfma-vgpr-form=true"]
     extra = os.environ.get("FA2_HIPCC_FLAGS")
     if extra:
         cmd += extra.split()

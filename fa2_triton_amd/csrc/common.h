@@ -32,6 +32,11 @@ typedef __attribute__((address_space(3))) char lds_char;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegInf = -__builtin_inff();
 
+// Defer-max threshold (log2 units): the running row max is only moved -- and O rescaled --
+// when some row of the wave grows by more than this; P then stays <= 2^kDeferMax, which fp32
+// accumulation and bf16/fp16 P (same relative precision at any magnitude) absorb exactly.
+constexpr float kDeferMax = 8.f;
+
 // ---------------------------------------------------------------------------------------------
 // Element traits: raw 16-bit storage, conversions and the matching MFMA.
 template <bool BF16>
@@ -268,6 +273,19 @@ struct Stager {
       const int gc = c < dchunks ? c : dchunks - 1;
       off[it] = (int32_t)(pr * row_stride) + gc * 8;
     }
+  }
+  // Branch-free single-piece issue for kernels that spread a tile's DMA over their steps
+  // (requires NTHREADS == ROWS * 4: every piece of a lane then lies in the same tile row, so
+  // one per-tile row clamp `adj` (elements, from row_adjust) serves all its pieces).
+  FA2_DEV int64_t row_adjust(int64_t row_stride, int row0, int row_end, int tid) const {
+    static_assert(NTHREADS == ROWS * 4, "one tile row per lane");
+    const int pr = ((tid & 63) + 64 * wave) >> 2;
+    const int over = row0 + pr - (row_end - 1);
+    return over > 0 ? -(int64_t)over * row_stride : 0;
+  }
+  FA2_DEV void piece(char* tile, const uint16_t* gt, int64_t adj, int it) const {
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds;
+    glds16(gt + off[it] + adj, base + it * NTHREADS * 16);
   }
   // rows [row0, row0 + ROWS) of g (row stride row_stride); rows >= row_end re-read row_end - 1
   FA2_DEV void issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int tid) {

@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "fa2_internal.h"
+#include "fwd_w64_kernel.h"
 
 namespace fa2 {
 
@@ -37,10 +38,13 @@ struct FwdCfg {
   static constexpr int kWavesPerSimd = DT >= 256 ? 1 : 2;
 };
 
-// Defer-max threshold (log2 units): the running row max is only moved -- and O rescaled --
-// when some row of the wave grows by more than this; P then stays <= 2^kDeferMax, which fp32
-// accumulation and bf16/fp16 P (same relative precision at any magnitude) absorb exactly.
-constexpr float kDeferMax = 8.f;
+
+#ifndef FA2_FWD_W64
+#define FA2_FWD_W64 0  // experimental one-wave-per-SIMD forward (fwd_w64_kernel.h)
+#endif
+#ifndef FA2_OLD_LEAD
+#define FA2_OLD_LEAD 3  // fragment reads in flight ahead of their MFMA (0: compiler order)
+#endif
 
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAUSAL>::kWavesPerSimd)) fwd_kernel(const fa2_fwd_args p) {
@@ -145,15 +149,35 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
   bool rescale = false;
 
   // QK^T + online softmax of one 64-key tile for this wave (MASK: diagonal / tail variant).
-  auto qk_softmax = [&](auto mask_c, const char* K, int n0) {
+  auto qk_softmax = [&](auto mask_c, const char* K, int n0, auto fill) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s[2];
+#if FA2_OLD_LEAD
+    {
+      // fenced steps: each fragment read runs FA2_OLD_LEAD MFMAs ahead, the two key halves'
+      // chains alternate
+      constexpr int N = 2 * KS, L = FA2_OLD_LEAD;
+      u32x4 kf[N];
+#pragma unroll
+      for (int j = 0; j < L; ++j) kf[j] = lds_row_frag<DT, BN>(K, 32 * (j & 1), r32, j >> 1, hh);
+      s[0] = zero16();
+      s[1] = zero16();
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        if (m + L < N) kf[m + L] = lds_row_frag<DT, BN>(K, 32 * ((m + L) & 1), r32, (m + L) >> 1, hh);
+        s[m & 1] = E::mfma(kf[m], qf[m >> 1], s[m & 1]);
+        fill(m);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       s[t] = zero16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) s[t] = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s[t]);
     }
+#endif
     // register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
     const int rel = lim_lane - n0 - 4 * hh;
     float mx = kNegInf;
@@ -218,6 +242,22 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
     }
+#if FA2_OLD_LEAD
+    {
+      constexpr int N = 4 * NDT, L = 2 * FA2_OLD_LEAD > N ? N : 2 * FA2_OLD_LEAD;
+      u32x4 vf[N];
+      auto rd = [&](int m) { return lds_tr_frag<DT, BN>(V, 16 * (m / NDT), 32 * (m % NDT), lane); };
+#pragma unroll
+      for (int j = 0; j < L; ++j) vf[j] = rd(j);
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        if (m + L < N) vf[m + L] = rd(m + L);
+        const int kk = m / NDT;
+        acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -225,29 +265,55 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp)
           acc[dt] = E::mfma(lds_tr_frag<DT, BN>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
+#endif
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
   __syncthreads();
 
+  constexpr int kPieces = Stager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
+  auto nofill = [](int) {};
+
   // Phase ph = 2 i + x: x = 0 (A_i) issues K_{i+1}, x = 1 (B_i) issues V_{i+1}.  A wave of
   // group g runs QK of tile (ph - g) / 2 when ph - g is even, PV of tile (ph - g - 1) / 2 when odd.
-  constexpr int kPieces = Stager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
   bool live = false;  // the pending PV of this wave has unmasked rows
   if constexpr (!PINGPONG) {
     // one barrier per tile: prefetch K/V_{i+1}, QK + softmax + PV of tile i
+    // With SPREAD the next tile's LDS-DMA pieces ride in the QK^T steps (one every other MFMA)
+    // instead of a burst at the top of the tile; rows past the end are clamped, so the issue
+    // is branch free (the last tile re-reads valid rows into a buffer nobody reads).
+    constexpr bool SPREAD = ALIGNED && FA2_OLD_LEAD && NT == BN * 4;
     for (int i = 0; i < ntiles; ++i) {
-      if (i + 1 < ntiles) {
+      const int n0 = i * BN;
+      const uint16_t* kgt = kg + (int64_t)(n0 + BN) * p.k_stride[1];
+      const uint16_t* vgt = vg + (int64_t)(n0 + BN) * p.v_stride[1];
+      int64_t kadj = 0, vadj = 0;
+      if constexpr (SPREAD) {
+        kadj = kst.row_adjust(p.k_stride[1], n0 + BN, Lk, tid);
+        vadj = vst.row_adjust(p.v_stride[1], n0 + BN, Lk, tid);
+      } else if (i + 1 < ntiles) {
         stage_k((i + 1) & 1, (i + 1) * BN);
         stage_v((i + 1) & 1, (i + 1) * BN);
       }
-      const int n0 = i * BN;
+      auto dma = [&](int pc) {
+        if (pc < kPieces) kst.piece(kt((i + 1) & 1), kgt, kadj, pc);
+        else vst.piece(vt((i + 1) & 1), vgt, vadj, pc - kPieces);
+      };
+      auto fill = [&](int m) {
+        if constexpr (SPREAD) {
+          constexpr int every = KS / kPieces;  // 2 QK steps per piece: K then V pieces
+          if (m % every == 0 && m / every < 2 * kPieces) dma(m / every);
+        }
+      };
       const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
       const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
       if (!dead) {
-        if (need_mask) qk_softmax(std::true_type{}, kt(i & 1), n0);
-        else qk_softmax(std::false_type{}, kt(i & 1), n0);
+        if (need_mask) qk_softmax(std::true_type{}, kt(i & 1), n0, fill);
+        else qk_softmax(std::false_type{}, kt(i & 1), n0, fill);
         pv_update(vt(i & 1));
+      } else if constexpr (SPREAD) {
+#pragma unroll
+        for (int pc = 0; pc < 2 * kPieces; ++pc) dma(pc);
       }
       vm_wait_all();
       __syncthreads();
@@ -272,8 +338,8 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
           const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
           live = !dead;
           if (!dead) {
-            if (need_mask) qk_softmax(std::true_type{}, kt(tile & 1), n0);
-            else qk_softmax(std::false_type{}, kt(tile & 1), n0);
+            if (need_mask) qk_softmax(std::true_type{}, kt(tile & 1), n0, nofill);
+            else qk_softmax(std::false_type{}, kt(tile & 1), n0, nofill);
           }
         }
       } else if (live) {
@@ -336,6 +402,11 @@ static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
 template <bool BF16, int DT>
 hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
+#if FA2_FWD_W64
+  if constexpr (DT == 64 || DT == 128) {
+    if (aligned && !bi && !dr) return c ? launch_fwd_w64<BF16, DT, true>(a, st) : launch_fwd_w64<BF16, DT, false>(a, st);
+  }
+#endif
 #define FA2_FWD_CASE(C, B, R, A)                                  \
   if (c == C && bi == B && dr == R && aligned == A)               \
     return launch_fwd_t<BF16, DT, C, B, R, A>(a, st);
