@@ -18,6 +18,15 @@
 #include "common.h"
 #include "fa2_internal.h"
 
+// k-steps of fragment reads in flight ahead of their MFMAs (0: compiler order); dK/dV runs at
+// the 256-register limit, where a second step in flight spills
+#ifndef FA2_DKDV_LEAD
+#define FA2_DKDV_LEAD 1
+#endif
+#ifndef FA2_DQ_LEAD
+#define FA2_DQ_LEAD 2
+#endif
+
 namespace fa2 {
 
 // ---------------------------------------------------------------------------------------------
@@ -153,6 +162,27 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
+#if FA2_DKDV_LEAD
+    {
+      // fenced steps, S and dP chains alternating, fragments read FA2_DKDV_LEAD k-steps ahead
+      constexpr int L = FA2_DKDV_LEAD < KS ? FA2_DKDV_LEAD : KS;
+      u32x4 fq[KS], fo[KS], fv[KS];
+      auto rd = [&](int ks) {
+        fq[ks] = lds_row_frag<DT, BMQ>(Q, 0, r32, ks, hh);
+        fo[ks] = lds_row_frag<DT, BMQ>(O, 0, r32, ks, hh);
+        fv[ks] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks, hh);
+      };
+#pragma unroll
+      for (int j = 0; j < L; ++j) rd(j);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + L < KS) rd(ks + L);
+        s = E::mfma(fq[ks], kf[ks], s);
+        dp = E::mfma(fo[ks], fv[ks], dp);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BMQ>(Q, 0, r32, ks, hh), kf[ks], s);
     __builtin_amdgcn_sched_barrier(0);
@@ -161,6 +191,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       dp = E::mfma(lds_row_frag<DT, BMQ>(O, 0, r32, ks, hh), lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks, hh), dp);
       if (ks & 1) __builtin_amdgcn_sched_barrier(0);  // at most two fragment pairs in flight
     }
+#endif
     __builtin_amdgcn_sched_barrier(0);
     // rows of register i: m + (i & 3) + 8 (i >> 2) + 4 hh.  The row window [q_lo, q_hi) of this
     // lane's key is recomputed from an opaque lane id: hoisted out of the loop it gets spilled
@@ -204,6 +235,27 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
     __builtin_amdgcn_sched_barrier(0);
+#if FA2_DKDV_LEAD
+    {
+      // steps m: dt = m % NDT (independent chains back to back), r = m / NDT: (sp, dV | dK)
+      constexpr int N = 4 * NDT, L = 2 * FA2_DKDV_LEAD < N ? 2 * FA2_DKDV_LEAD : N;
+      u32x4 fr[N];
+      auto rd = [&](int m) {
+        const int dt = m % NDT, r = m / NDT;
+        return lds_tr_frag<DT, BMQ>((r & 1) ? Q : O, 16 * (r >> 1), 32 * dt, lane);
+      };
+#pragma unroll
+      for (int j = 0; j < L; ++j) fr[j] = rd(j);
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        if (m + L < N) fr[m + L] = rd(m + L);
+        const int dt = m % NDT, r = m / NDT;
+        if (r & 1) dk[dt] = E::mfma(fr[m], dsp[r >> 1], dk[dt]);
+        else dv[dt] = E::mfma(fr[m], pp[r >> 1], dv[dt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#else
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
@@ -213,6 +265,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       }
       __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
     }
+#endif
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
@@ -384,11 +437,31 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     for (int t = 0; t < 2; ++t) {
       if (MASK && !(n0 + 32 * t < Lk && (!CAUSAL || n0 + 32 * t <= mw0 + 31 + diag))) continue;
       f32x16 s = zero16(), dp = zero16();
+#if FA2_DQ_LEAD
+      {
+        constexpr int L = FA2_DQ_LEAD < KS ? FA2_DQ_LEAD : KS;
+        u32x4 fk[KS], fv[KS];
+        auto rd = [&](int ks) {
+          fk[ks] = lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh);
+          fv[ks] = lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh);
+        };
+#pragma unroll
+        for (int j = 0; j < L; ++j) rd(j);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + L < KS) rd(ks + L);
+          s = E::mfma(fk[ks], qf[ks], s);
+          dp = E::mfma(fv[ks], of[ks], dp);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       u32x4 dsp[2];
 #pragma unroll
@@ -414,6 +487,21 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
         for (int j = 0; j < 4; ++j) dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
       }
       __builtin_amdgcn_sched_barrier(0);
+#if FA2_DQ_LEAD
+      {
+        constexpr int N = 2 * NDT, L = 2 * FA2_DQ_LEAD < N ? 2 * FA2_DQ_LEAD : N;
+        u32x4 fr[N];
+        auto rd = [&](int m) { return lds_tr_frag<DT, BN>(K, 32 * t + 16 * (m / NDT), 32 * (m % NDT), lane); };
+#pragma unroll
+        for (int j = 0; j < L; ++j) fr[j] = rd(j);
+#pragma unroll
+        for (int m = 0; m < N; ++m) {
+          if (m + L < N) fr[m + L] = rd(m + L);
+          acc[m % NDT] = E::mfma(fr[m], dsp[m / NDT], acc[m % NDT]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
@@ -421,6 +509,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           acc[dt] = E::mfma(lds_tr_frag<DT, BN>(K, 32 * t + 16 * sp, 32 * dt, lane), dsp[sp], acc[dt]);
         if (dt & 1) __builtin_amdgcn_sched_barrier(0);
       }
+#endif
     }
   };
 
