@@ -105,7 +105,6 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
   if (rc) return rc;
-  if (a->dropout_p > 0.f) return fail(FA2_E_UNSUPPORTED, "Backward pass does not yet support dropout.");
   if (!a->q || !a->k || !a->v || !a->o || !a->dout || !a->lse || !a->delta || !a->dq || !a->dk || !a->dv)
     return fail(FA2_E_INVALID, "null tensor pointer");
   if (a->dq_dtype != a->dtype && a->dq_dtype != FA2_F32) return fail(FA2_E_INVALID, "dq dtype %d", a->dq_dtype);

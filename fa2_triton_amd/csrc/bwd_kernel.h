@@ -23,6 +23,9 @@
 #ifndef FA2_DKDV_LEAD
 #define FA2_DKDV_LEAD 1
 #endif
+#ifndef FA2_DKDV_ABL
+#define FA2_DKDV_ABL 0  // timing ablations of dK/dV: 1 = no P/dS VALU, 2 = no Q/dO prefetch
+#endif
 #ifndef FA2_DQ_LEAD
 #define FA2_DQ_LEAD 2
 #endif
@@ -74,7 +77,7 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 //   dK^T[d][key] += Q^T dS  NDT*2 MFMA
 // dK/dV accumulate the whole GQA group in fp32 and are rounded once.  <= 256 VGPRs, so two
 // workgroups share a CU (DT <= 128).
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NT = 256;
@@ -104,6 +107,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   const bool kval = kj < Lk;
   const float scale = p.softmax_scale, scale2 = scale * kLog2e;
   const float sc = BIAS ? 1.f : scale2;
+  // dropout: flat Philox offset of (b, hq, row, key) exactly as the forward (fwd_kernel.h)
+  const int cu0 = p.cu_seqlens ? p.cu_seqlens[b] : 0;
+  auto drop_base = [&](int hq_) -> uint64_t {
+    return (uint64_t)Lk * ((uint64_t)cu0 + (uint64_t)Lq * ((uint64_t)hq_ + (uint64_t)p.heads_q * (p.cu_seqlens ? 0 : b)));
+  };
+  const float inv_keep = DROPOUT ? 1.f / (1.f - p.dropout_p) : 1.f;
 
   char* Vs = smem;
   auto qt = [&](int buf) { return smem + VT + buf * 2 * QT; };
@@ -224,10 +233,25 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
           x = fmaf(x, scale2, kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
                                                            (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype));
         }
+#if FA2_DKDV_ABL & 1
+        pv[j] = x;
+        dsv[j] = dp[i];
+#else
         float pr = __builtin_amdgcn_exp2f(fmaf(x, sc, -l4[j]));
         if (MASK) pr = (o >= lo && o < hi) ? pr : 0.f;
-        pv[j] = pr;
-        dsv[j] = pr * (dp[i] - d4[j]);  // softmax_scale is applied to dK once, at the end
+        if (DROPOUT) {
+          // the forward's keep mask (same Philox offsets), P~ = P M / (1 - p):
+          // dV += P~^T dO, dS = P (dP~ M / (1 - p) - delta)
+          const uint64_t qr = (uint64_t)(m + o + 4 * hh);
+          const bool keep = philox_uniform(p.dropout_seed, drop_base(hq) + qr * (uint64_t)Lk + (uint64_t)kj) > p.dropout_p;
+          const float kp = keep ? inv_keep : 0.f;
+          pv[j] = pr * kp;
+          dsv[j] = pr * (dp[i] * kp - d4[j]);
+        } else {
+          pv[j] = pr;
+          dsv[j] = pr * (dp[i] - d4[j]);  // softmax_scale is applied to dK once, at the end
+        }
+#endif
       }
       pp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(pv[0], pv[1]);
       pp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(pv[2], pv[3]);
@@ -284,7 +308,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
+#if !(FA2_DKDV_ABL & 2)
     if (step + 1 < total) stage(step + 1, cur ^ 1);
+#endif
     const int g = step / n_mt, mt = step - g * n_mt;
     const int hq = hkv * G + g;
     const int m = m_begin + mt * BMQ;
@@ -345,7 +371,7 @@ struct DqCfg {
 // LDS (double buffered).  Per tile and wave:
 //   S^T, dP^T [key][q]   2 x (8 + 8) MFMA (A = K / V row fragments, B = Q / dO in VGPRs)
 //   dQ^T[d][q] += K^T dS^T   NDT*4 MFMA (A = K^T via ds_read_b64_tr_b16)
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED, bool DQF32>
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED, bool DQF32>
 __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) dq_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NW = DqCfg<DT>::NW;
@@ -427,6 +453,15 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + diag + 1) : Lk);
   const float sc = BIAS ? 1.f : scale2;
   const float nlse = -lse_i;
+  // dropout: Philox offset of (b, hq, qi, key 0), as the forward (fwd_kernel.h)
+  uint64_t drop_row = 0;
+  float inv_keep = 1.f;
+  if (DROPOUT) {
+    const uint64_t cu0 = p.cu_seqlens ? (uint64_t)p.cu_seqlens[b] : 0;
+    drop_row = (uint64_t)Lk * (cu0 + (uint64_t)Lq * ((uint64_t)hq + (uint64_t)p.heads_q * (p.cu_seqlens ? 0 : b))) +
+               (uint64_t)qi * (uint64_t)Lk;
+    inv_keep = 1.f / (1.f - p.dropout_p);
+  }
 
   // one 64-key tile: S^T and dP^T for both 32-key halves first, then the softmax-gradient
   // VALU of each half beside the other half's MFMAs, then dQ^T += K^T dS^T.
@@ -481,7 +516,13 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           }
           float pr = __builtin_amdgcn_exp2f(fmaf(x, sc, nlse));
           if (MASK) pr = o < rel ? pr : 0.f;
-          dsv[j] = pr * (dp[i] - del_i);  // softmax_scale is applied to dQ once, at the end
+          if (DROPOUT) {  // dS = P (dP~ M / (1 - p) - delta), the forward's keep mask M
+            const uint64_t kjj = (uint64_t)(n0 + o + 4 * hh);
+            const bool keep = philox_uniform(p.dropout_seed, drop_row + kjj) > p.dropout_p;
+            dsv[j] = pr * (dp[i] * (keep ? inv_keep : 0.f) - del_i);
+          } else {
+            dsv[j] = pr * (dp[i] - del_i);  // softmax_scale is applied to dQ once, at the end
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
@@ -565,7 +606,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 }
 
 // ---------------------------------------------------------------------------------------------
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool ALIGNED>
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
   if (stages & 1) {
     dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
@@ -573,32 +614,32 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   }
   if (stages & 2) {
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if (stages & 4) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
     dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
     else
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
+      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
   return hipGetLastError();
 }
 
 template <bool BF16, int DT>
 hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStream_t st) {
-  const bool c = a.causal != 0, bi = a.bias != nullptr;
-#define FA2_BWD_CASE(C, B, A) \
-  if (c == C && bi == B && aligned == A) return launch_bwd_t<BF16, DT, C, B, A>(a, stages, st);
-  FA2_BWD_CASE(true, true, true)
-  FA2_BWD_CASE(true, true, false)
-  FA2_BWD_CASE(true, false, true)
-  FA2_BWD_CASE(true, false, false)
-  FA2_BWD_CASE(false, true, true)
-  FA2_BWD_CASE(false, true, false)
-  FA2_BWD_CASE(false, false, true)
-  FA2_BWD_CASE(false, false, false)
+  const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
+#define FA2_BWD_CASE(C, B, R, A) \
+  if (c == C && bi == B && dr == R && aligned == A) return launch_bwd_t<BF16, DT, C, B, R, A>(a, stages, st);
+#define FA2_BWD_A(C, B, R) FA2_BWD_CASE(C, B, R, true) FA2_BWD_CASE(C, B, R, false)
+#define FA2_BWD_R(C, B) FA2_BWD_A(C, B, true) FA2_BWD_A(C, B, false)
+  FA2_BWD_R(true, true)
+  FA2_BWD_R(true, false)
+  FA2_BWD_R(false, true)
+  FA2_BWD_R(false, false)
+#undef FA2_BWD_R
+#undef FA2_BWD_A
 #undef FA2_BWD_CASE
   return hipErrorInvalidValue;
 }

@@ -275,11 +275,12 @@ struct Stager {
     }
   }
   // Branch-free single-piece issue for kernels that spread a tile's DMA over their steps
-  // (requires NTHREADS == ROWS * 4: every piece of a lane then lies in the same tile row, so
-  // one per-tile row clamp `adj` (elements, from row_adjust) serves all its pieces).
+  // (requires NTHREADS % (ROWS * 4) == 0: piece it of a lane is it * NTHREADS + tid, so all
+  // its pieces lie in tile row (tid % (ROWS * 4)) / 4 and one per-tile row clamp `adj`
+  // (elements, from row_adjust) serves them all).
   FA2_DEV int64_t row_adjust(int64_t row_stride, int row0, int row_end, int tid) const {
-    static_assert(NTHREADS == ROWS * 4, "one tile row per lane");
-    const int pr = ((tid & 63) + 64 * wave) >> 2;
+    static_assert(NTHREADS % (ROWS * 4) == 0, "one tile row per lane");
+    const int pr = (tid % (ROWS * 4)) >> 2;
     const int over = row0 + pr - (row_end - 1);
     return over > 0 ? -(int64_t)over * row_stride : 0;
   }

@@ -44,14 +44,21 @@ def infer_bias_strides(
 
 
 def handle_dropout(dropout_p: float, dropout_seed: Optional[int], is_forward: bool) -> int:
-    """Seed handling of /root/reference/src/utils.py:80-88 (backward dropout unsupported)."""
+    """Seed handling of /root/reference/src/utils.py:80-88.
+
+    The reference raises NotImplementedError for a backward with dropout (:88); here the
+    backward kernels regenerate the forward's Philox keep mask,
+    so the backward only needs the seed the forward used.
+    """
     assert dropout_p >= 0, f"Dropout probability {dropout_p = } must be above 0."
     assert dropout_p < 1, f"Dropout probability {dropout_p = } must be strictly below 1."
     if dropout_p == 0:
         return 0
     if is_forward:
         return torch.randint(low=0, high=2**32, size=(1,)).item() if dropout_seed is None else dropout_seed
-    raise NotImplementedError("Backward pass does not yet support dropout.")
+    if dropout_seed is None:
+        raise ValueError("a backward with dropout needs the dropout_seed its forward used")
+    return dropout_seed
 
 
 def encode_dtype(x: Tensor) -> int:

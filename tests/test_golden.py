@@ -84,7 +84,7 @@ def test_kernels_match_golden(name, dtype):
     err = (out.float() - ref_out).abs().max().item()
     err_pt = (pt.float() - ref_out).abs().max().item()
     assert err <= 2 * err_pt + 5e-5, (err, err_pt)
-    if m["p"] == 0:
+    if True:  # with dropout too: the backward regenerates the forward's keep mask
         grads = torch.autograd.grad(out, (q, k, v), do)
         grads_pt = torch.autograd.grad(pt, (q, k, v), do)
         for nm, gg, gp in zip(("dq", "dk", "dv"), grads, grads_pt):

@@ -58,7 +58,9 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fa2_fwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID
     b = _lib.BwdArgs()
     b.batch, b.heads_q, b.heads_kv, b.seqlen_q, b.seqlen_k, b.head_dim = 1, 2, 2, 16, 16, 64
-    b.dtype, b.dq_dtype, b.lse_row_stride, b.dropout_p = _lib.FA2_F16, _lib.FA2_F16, 128, 0.1
+    b.dtype, b.dq_dtype, b.lse_row_stride, b.dropout_p = _lib.FA2_F16, _lib.FA2_F16, 128, 1.5
+    assert lib.fa2_bwd(ctypes.byref(b), None) == _lib.FA2_E_INVALID
+    b.dropout_p, b.head_dim = 0.1, 300
     assert lib.fa2_bwd(ctypes.byref(b), None) == _lib.FA2_E_UNSUPPORTED
     with pytest.raises(NotImplementedError):
         _lib.check(_lib.FA2_E_UNSUPPORTED)
@@ -80,8 +82,9 @@ def test_handle_dropout_and_dtype_codes():
     assert handle_dropout(0.0, None, True) == 0
     assert handle_dropout(0.1, 1234, True) == 1234
     assert 0 <= handle_dropout(0.1, None, True) < 2**32
-    with pytest.raises(NotImplementedError):
-        handle_dropout(0.1, 1, False)
+    assert handle_dropout(0.1, 77, False) == 77  # backward regenerates the forward's mask
+    with pytest.raises(ValueError):
+        handle_dropout(0.1, None, False)
     with pytest.raises(AssertionError):
         handle_dropout(1.0, None, True)
     assert encode_dtype(torch.zeros(1, dtype=torch.float16)) == 16
