@@ -1,0 +1,93 @@
+"""Context numbers: this operator vs torch.nn.functional.scaled_dot_product_attention on ROCm.
+
+SURVEY.md section 8(f) rank 4 (the reference's own comparison harness is
+/root/reference/benchmarks/utils.py:22-93 against FlexAttention, src/other_implementations/).
+Both sides get the same synthetic N(0, 0.5) bf16/fp16 inputs resident in HBM; SDPA gets
+contiguous [B, H, S, D] tensors (its native layout), ours the reference's [B, S, H, D].
+Times are medians of HIP-event-timed calls after warmup; TFLOP/s use the algorithmic count of
+SURVEY.md section 8(d) (fwd 4 B H S^2 D, x0.5 causal; bwd 2.5x fwd).
+
+usage: python scripts/compare_sdpa.py [--reps 20]   (prints one JSON line per config)
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fa2_triton_amd import flash_attn_func  # noqa: E402
+
+CONFIGS = [
+    # name, B, Hq, Hkv, S, D, causal, dtype
+    ("cfg2", 8, 16, 16, 1024, 64, False, torch.bfloat16),
+    ("cfg3", 8, 32, 32, 4096, 128, True, torch.bfloat16),
+    ("cfg3-noncausal", 8, 32, 32, 4096, 128, False, torch.bfloat16),
+    ("cfg5-gqa", 2, 32, 8, 8192, 128, True, torch.float16),
+]
+
+
+def timed(fn, reps, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    for name, b, hq, hkv, s, d, causal, dtype in CONFIGS:
+        fl = 4 * b * hq * s * s * d * (0.5 if causal else 1.0)
+        q = torch.empty(b, s, hq, d, device="cuda", dtype=dtype).normal_(0, 0.5).requires_grad_()
+        k = torch.empty(b, s, hkv, d, device="cuda", dtype=dtype).normal_(0, 0.5).requires_grad_()
+        v = torch.empty(b, s, hkv, d, device="cuda", dtype=dtype).normal_(0, 0.5).requires_grad_()
+        do = torch.randn_like(q)
+        qs, ks, vs = (t.detach().transpose(1, 2).contiguous().requires_grad_() for t in (q, k, v))
+        dos = do.transpose(1, 2).contiguous()
+        gqa = {"enable_gqa": True} if hkv != hq else {}
+
+        def ours_fwd():
+            with torch.no_grad():
+                flash_attn_func(q, k, v, None, None, 0.0, causal)
+
+        def ours_fwdbwd():
+            o = flash_attn_func(q, k, v, None, None, 0.0, causal)
+            torch.autograd.grad(o, (q, k, v), do)
+
+        def sdpa_fwd():
+            with torch.no_grad():
+                F.scaled_dot_product_attention(qs, ks, vs, is_causal=causal, **gqa)
+
+        def sdpa_fwdbwd():
+            o = F.scaled_dot_product_attention(qs, ks, vs, is_causal=causal, **gqa)
+            torch.autograd.grad(o, (qs, ks, vs), dos)
+
+        row = {"config": name, "B": b, "Hq": hq, "Hkv": hkv, "S": s, "D": d, "causal": causal,
+               "dtype": str(dtype).replace("torch.", "")}
+        for tag, fn, mult in (("ours_fwd", ours_fwd, 1.0), ("ours_fwdbwd", ours_fwdbwd, 3.5),
+                              ("sdpa_fwd", sdpa_fwd, 1.0), ("sdpa_fwdbwd", sdpa_fwdbwd, 3.5)):
+            try:
+                ms = timed(fn, args.reps)
+                row[tag + "_ms"] = round(ms, 4)
+                row[tag + "_tflops"] = round(fl * mult / ms / 1e9, 1)
+            except Exception as exc:  # e.g. a backend without GQA support
+                row[tag + "_error"] = f"{type(exc).__name__}: {exc}"[:200]
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
