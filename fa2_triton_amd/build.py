@@ -62,11 +62,19 @@ def compile_one(src: str, force: bool, dep_t: float) -> str:
     obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(dep_t, os.path.getmtime(src)):
         return obj
+    # development A/B builds: FA2_BUILD_ONLY=fwd_bf16_d128,... recompiles only those units and
+    # keeps every other existing object as it is
+    only = os.environ.get("FA2_BUILD_ONLY")
+    if only and os.path.exists(obj) and not any(tok in os.path.basename(src) for tok in only.split(",")):
+        return obj
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
            "-I", CSRC, "-I", INCLUDE, "-Wno-unused-result",
            # MFMA accumulators in arch VGPRs: at one wave per SIMD (fwd_w64_kernel.h) the
            # default heuristic puts them in AGPRs and copies the O tile through VGPRs per tile
-           "-mllvm", "-amdgpu-mfma-vgpr-form=true"]
+           "-mllvm", "-amdgpu-mfma-vgpr-form=true",
+           # no SLP packing of the softmax adds into v_pk_add_f32: packed f32 VALU beside MFMAs
+           # costs more issue cycles than the scalar pair (MI355X_MICROARCH.md, filler prices)
+           "-fno-slp-vectorize"]
     extra = os.environ.get("FA2_HIPCC_FLAGS")
     if extra:
         cmd += extra.split()

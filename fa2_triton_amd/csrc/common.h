@@ -312,6 +312,67 @@ struct Stager {
   }
 };
 
+// Buffer-resource LDS-DMA stager (buffer_load_dwordx4 ... lds) for a ROWS x DT tile.  The
+// descriptor of each tile starts at the tile's first row and its range ends at the last valid
+// row, so rows past the end read as zeros by the hardware range check: no clamping and no
+// per-piece address arithmetic -- every lane's byte offset of its piece is a constant.
+// Requires NTHREADS % (ROWS * 4) == 0 (all pieces of a lane in one tile row).
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+FA2_DEV i32x4 make_rsrc(const void* base, uint32_t n) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int32_t)((uint32_t)(a >> 32) & 0xFFFFu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int32_t)n);
+  r[3] = 0x00020000;  // gfx9 raw buffer: 32-bit data, no swizzle
+  return r;
+}
+
+template <int DT, int ROWS, int NTHREADS>
+struct BufStager {
+  static constexpr int kPieces = ROWS * DT / 8;
+  static constexpr int kIters = (kPieces + NTHREADS - 1) / NTHREADS;
+  static_assert(kPieces % NTHREADS == 0 && NTHREADS % (ROWS * 4) == 0, "one tile row per lane");
+  uint32_t voff[kIters];  // byte offset of this lane's pieces from the tile's first row
+  uint32_t wave_lds;      // byte offset of this wave's first piece in the tile (SGPR)
+
+  FA2_DEV void init(int tid, int64_t row_stride, int D) {
+    const int wave = tid >> 6, lane = tid & 63, dchunks = D >> 3;
+    wave_lds = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int piece = (it * (NTHREADS / 64) + wave) * 64 + lane;
+      const int sub = piece / (ROWS * 4), within = piece % (ROWS * 4);
+      const int pr = within >> 2;
+      const int c = sub * 4 + ((within & 3) ^ ((pr >> 2) & 3));
+      const int gc = c < dchunks ? c : dchunks - 1;
+      voff[it] = (uint32_t)(pr * row_stride + gc * 8) * 2u;
+    }
+  }
+  // descriptor of the tile starting at row row0 of g (rows >= row_end read as zero)
+  // (max_rows = rows whose bytes fit the 32-bit range field, see max_rows())
+  FA2_DEV static i32x4 tile_rsrc(const uint16_t* g, int64_t row_stride, int row0, int row_end, int max_rows) {
+    const int rows = min(max(row_end - row0, 0), max_rows);
+    return make_rsrc(g + (int64_t)row0 * row_stride, (uint32_t)rows * (uint32_t)(row_stride * 2));
+  }
+  FA2_DEV static int max_rows(int64_t row_stride) { return (int)min((int64_t)0x7FFFFFFF, 0xFFFFFFFFll / (row_stride * 2)); }
+  FA2_DEV void piece(char* tile, i32x4 rsrc, int it) const {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds + it * NTHREADS * 16;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff[it]), "s"(rsrc), "s"(lds)
+        : "memory");
+  }
+  FA2_DEV void issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int max_rows) const {
+    const i32x4 r = tile_rsrc(g, row_stride, row0, row_end, max_rows);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) piece(tile, r, it);
+  }
+};
+
 // 16-byte register fragment straight from global memory: elements [d0, d0 + 8) of one row;
 // zero outside [0, D) or when !valid.
 template <bool ALIGNED>

@@ -1,0 +1,359 @@
+// fwd_pipe_kernel.h -- software-pipelined FlashAttention-2 forward for gfx950 (the hot path:
+// aligned head dim, no bias, no dropout).  Same semantics as fwd_kernel (fwd_kernel.h) and the
+// reference's _fwd_kernel / compute_row_block (/root/reference/src/forward/kernel.py:61-291,
+// /root/reference/src/forward/compute_row_blocks.py:7-103).
+//
+// Work decomposition as fwd_kernel's causal path: 4 waves x 32 query rows per workgroup, two
+// workgroups per CU, 64-key K/V tiles double buffered in LDS by LDS-DMA, one barrier per tile.
+//
+// What is different is the order of work inside a wave.  fwd_kernel runs
+//   QK^T(i) -> softmax(i) -> PV(i)
+// so a wave's softmax (~110 VALU ops, 32 of them v_exp) has no MFMA of its own to hide behind.
+// Here the wave keeps the raw scores of the NEXT tile in registers and every iteration runs two
+// fenced phases:
+//   phase X: QK^T(i+1) MFMAs, each step carrying two exponentials, the row-sum adds and one
+//            bf16 pack of softmax(i), plus one LDS-DMA piece every other step;
+//   phase Y: PV(i) MFMAs, each step carrying one v_max3 of the row max of S(i+1).
+// The defer-max decision for tile i+1 (one wave vote) and the rare O rescale sit between
+// iterations.  The LDS schedule shifts K by one tile: iteration i reads K(i+1) and V(i) while
+// K(i+2) and V(i+1) land in the buffers K(i) and V(i-1) vacated in iteration i-1.
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+
+namespace fa2 {
+
+#ifndef FA2_FWD_PIPE
+#define FA2_FWD_PIPE 2
+#endif
+
+template <bool BF16, int DT, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int NW = 4, NT = NW * 64;
+  constexpr int BM = NW * 32;        // query rows per workgroup
+  constexpr int BN = 64;             // keys per tile
+  constexpr int KS = DT / 16;        // k-steps of Q K^T
+  constexpr int NDT = DT / 32;       // 32-wide d tiles of O
+  constexpr int NQK = 2 * KS;        // QK^T MFMA steps per tile (two 32-key halves)
+  constexpr int NPV = 4 * NDT;       // PV MFMA steps per tile
+  constexpr int EPS = 32 / NQK;      // exponentials per QK^T step
+  constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
+  constexpr int LEAD = 3;            // fragment reads in flight ahead of their MFMA
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
+  static_assert(NQK % 8 == 0 && 32 % NQK == 0, "QK^T steps must carry whole pack pairs");
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
+  const int r32 = lane & 31, hh = lane >> 5;
+
+  // ---- work item (as fwd_kernel: head-major per XCD, heaviest first) -----------------------
+  const int nmb = (p.seqlen_q + BM - 1) / BM;
+  const int item = xcd_item(blockIdx.x, gridDim.x);
+  const int bh = item / nmb;
+  const int mbi = item - bh * nmb;
+  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;
+  const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
+  const int hkv = hq / (p.heads_q / p.heads_kv);
+  int Lq = p.seqlen_q, Lk = p.seqlen_k;
+  if (p.cu_seqlens) {
+    const int cu = p.cu_seqlens[b];
+    Lq = Lk = p.cu_seqlens[b + 1] - cu;
+  }
+  const int m0 = mb * BM;
+  const int qw0 = m0 + w * 32;  // first row of this wave
+  const int qi = qw0 + r32;     // this lane's query row
+  const int D = p.head_dim;
+
+  const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
+  const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
+  const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
+
+  int n_end = 0;
+  if (m0 < Lq) {
+    n_end = Lk;
+    if (CAUSAL) n_end = min(Lk, m0 + BM + Lk - Lq);
+    n_end = max(n_end, 0);
+  }
+  const int ntiles = (n_end + BN - 1) / BN;
+  const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
+
+  auto kt = [&](int buf) { return smem + buf * TILE; };
+  auto vt = [&](int buf) { return smem + (2 + buf) * TILE; };
+  BufStager<DT, BN, NT> kst;  // K and V share row strides (checked by the launcher): one offset set
+  kst.init(tid, p.k_stride[1], D);
+  const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
+  if (ntiles > 0) {
+    kst.issue(kt(0), kg, p.k_stride[1], 0, Lk, mrows);
+    kst.issue(vt(0), vg, p.v_stride[1], 0, Lk, mrows);
+    if (ntiles > 1) kst.issue(kt(1), kg, p.k_stride[1], BN, Lk, mrows);
+  }
+
+  // ---- Q fragments (B operand of S^T = K Q^T) ------------------------------------------------
+  u32x4 qf[KS];
+  {
+    const bool qvalid = qi < Lq;
+    const uint16_t* qrow = qg + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = load_row_frag<true>(qrow, 16 * ks + 8 * hh, D, qvalid);
+  }
+
+  const float sc = p.softmax_scale * kLog2e;
+  float m_run = kNegInf, l_run = 0.f;
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
+
+  // per-lane key limit: key kj is visible to this lane's row iff kj < lim_lane
+  const int lim_lane = CAUSAL ? min(Lk, qi + diag + 1) : Lk;
+  // wave-uniform tile classes
+  auto tile_live = [&](int t) { return t < ntiles && !(CAUSAL && t * BN > qw0 + 31 + diag); };
+  auto tile_mask = [&](int t) { return (t * BN + BN > Lk) || (CAUSAL && t * BN + BN - 1 > qw0 + diag); };
+
+  f32x16 s[2];   // raw scores S^T of the tile whose softmax is next
+  float mx = kNegInf;  // their (masked) row max, both lane halves combined, times sc
+  u32x4 pf[2][2];      // P of the current tile, packed: B operand of O^T += V^T P^T
+
+  // masked raw scores + row max (register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh)
+  auto mask_max = [&](int n0) {
+    const int rel = lim_lane - n0 - 4 * hh;
+    float m = kNegInf;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int o = 32 * t + (i & 3) + 8 * (i >> 2);
+        s[t][i] = o < rel ? s[t][i] : kNegInf;
+        m = fmaxf(m, s[t][i]);
+      }
+    mx = half_max(m) * sc;
+  };
+  auto plain_max = [&]() {
+    float m0_ = kNegInf, m1_ = kNegInf;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      m0_ = fmaxf(m0_, s[0][i]);
+      m1_ = fmaxf(m1_, s[1][i]);
+    }
+    mx = half_max(fmaxf(m0_, m1_)) * sc;
+  };
+  auto kfrag = [&](const char* K, int m) { return lds_row_frag<DT, BN>(K, 32 * (m & 1), r32, m >> 1, hh); };
+  auto vfrag = [&](const char* V, int m) { return lds_tr_frag<DT, BN>(V, 16 * (m / NDT), 32 * (m % NDT), lane); };
+
+  // QK^T of one tile into s (no interleaved work)
+  auto qk_plain = [&](const char* K) {
+    u32x4 kf[NQK];
+#pragma unroll
+    for (int j = 0; j < LEAD; ++j) kf[j] = kfrag(K, j);
+    s[0] = zero16();
+    s[1] = zero16();
+#pragma unroll
+    for (int m = 0; m < NQK; ++m) {
+      if (m + LEAD < NQK) kf[m + LEAD] = kfrag(K, m + LEAD);
+      s[m & 1] = E::mfma(kf[m], qf[m >> 1], s[m & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // defer-max decision for the scores in s; returns m_use, rescales O when the max moved
+  auto softmax_begin = [&]() {
+    const bool rescale = !__all(mx - m_run <= kDeferMax);
+    const float m_new = rescale ? fmaxf(m_run, mx) : m_run;
+    const float m_use = m_new == kNegInf ? 0.f : m_new;
+    if (rescale) {
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+    }
+    m_run = m_new;
+    return m_use;
+  };
+
+  // exponentials e..e+1 of the flat 32-score list -> P, row-sum partials
+  auto exp_pair = [&](const f32x16* src, int e, float m_use, float& rs0, float& rs1) {
+    const int t = e >> 4, i = e & 15;
+#ifdef FA2_EXP_NOEXP
+    const float p0 = fmaf(src[t][i], sc, -m_use);
+    const float p1 = fmaf(src[t][i + 1], sc, -m_use);
+#else
+    const float p0 = __builtin_amdgcn_exp2f(fmaf(src[t][i], sc, -m_use));
+    const float p1 = __builtin_amdgcn_exp2f(fmaf(src[t][i + 1], sc, -m_use));
+#endif
+    rs0 += p0;
+    rs1 += p1;
+    pf[t][i >> 3][(i & 7) >> 1] = E::pack2(p0, p1);
+  };
+
+  __builtin_amdgcn_s_waitcnt(0);  // Q fragments + K0, V0, K1
+  __syncthreads();
+
+  // prologue: S(0)
+  if (tile_live(0)) {
+    qk_plain(kt(0));
+    if (tile_mask(0)) mask_max(0);
+    else plain_max();
+  }
+  __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
+
+  constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
+  constexpr int kEvery = NQK / (2 * kPieces) > 0 ? NQK / (2 * kPieces) : 1;
+
+  // DMA targets of iteration i: K(i+2) -> K buffer i&1, V(i+1) -> V buffer (i+1)&1.  Rows
+  // past the end read as zeros (buffer range check); tiles wholly past it land in buffers
+  // nobody reads again.
+  auto dma = [&](int i, int pc) {
+    if (pc < kPieces) {
+      kst.piece(kt(i & 1), BufStager<DT, BN, NT>::tile_rsrc(kg, p.k_stride[1], (i + 2) * BN, Lk, mrows), pc);
+    } else {
+      kst.piece(vt((i + 1) & 1), BufStager<DT, BN, NT>::tile_rsrc(vg, p.v_stride[1], (i + 1) * BN, Lk, mrows),
+                pc - kPieces);
+    }
+  };
+
+  // Steady-state iterations of this wave: tile i live and tile i+1 live and unmasked.  The
+  // count differs between the waves of a workgroup (causal diagonal), so each wave runs its own
+  // two loops; every iteration of either loop ends in the same one barrier, and the waves stay
+  // in step by iteration index.
+  int n_full = Lk / BN;  // leading tiles that need no mask for any row of this wave
+  if (CAUSAL) n_full = min(n_full, qw0 + diag + 1 >= 0 ? (qw0 + diag + 1) / BN : 0);
+  const int n_steady = max(0, min(n_full, ntiles) - 1);
+
+  // One steady iteration: softmax of the scores in cur, QK^T(i+1) into nxt.  Unrolled by two
+  // with the roles of the two score arrays swapped, so no register copies between iterations.
+  f32x16 s2[2];
+  // QK: tile i+1 is live for this wave; MASK: it needs the causal / key-tail mask.
+  auto step = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto mask_c) {
+    constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value;
+    const char* K1 = kt((i + 1) & 1);
+    const char* V0 = vt(i & 1);
+    // phase X: QK^T(i+1) with softmax(i) and the DMA pieces riding along.  One key half after
+    // the other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume
+    // cur[0] then cur[1]: 48 score registers live at any step, not 64.
+    {
+      const float m_use = softmax_begin();
+      float rs0 = 0.f, rs1 = 0.f;
+      u32x4 kf[NQK];
+      auto kfs = [&](int m) { return kfrag(K1, 2 * (m % KS) + m / KS); };
+      if constexpr (QK) {
+#pragma unroll
+        for (int j = 0; j < LEAD; ++j) kf[j] = kfs(j);
+      }
+#pragma unroll
+      for (int m = 0; m < NQK; ++m) {
+        if constexpr (QK) {
+          if (m + LEAD < NQK) kf[m + LEAD] = kfs(m + LEAD);
+          const int t = m / KS, ks = m % KS;
+          nxt[t] = E::mfma(kf[m], qf[ks], ks == 0 ? zero16() : nxt[t]);
+        }
+#pragma unroll
+        for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, m_use, rs0, rs1);
+#ifndef FA2_EXP_NODMA
+        if (m % kEvery == 0 && m / kEvery < 2 * kPieces) dma(i, m / kEvery);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      l_run += rs0 + rs1;
+    }
+    // phase Y: PV(i) with the row max of S(i+1), one v_max3 per step
+    {
+      constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
+      constexpr int PER = 32 / NPV;
+      u32x4 vf[NPV];
+      float ma = kNegInf, mb_ = kNegInf;
+      const int rel = lim_lane - (i + 1) * BN - 4 * hh;
+#pragma unroll
+      for (int j = 0; j < L; ++j) vf[j] = vfrag(V0, j);
+#pragma unroll
+      for (int m = 0; m < NPV; ++m) {
+        if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
+        const int kk = m / NDT;
+        acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
+        if constexpr (QK) {
+#pragma unroll
+          for (int e = m * PER; e < (m + 1) * PER; ++e) {
+            const int t = e >> 4, r = e & 15;
+            if constexpr (MASK) {
+              const int o = 32 * t + (r & 3) + 8 * (r >> 2);
+              nxt[t][r] = o < rel ? nxt[t][r] : kNegInf;
+            }
+            float& mm = t ? mb_ : ma;
+            mm = fmaxf(mm, nxt[t][r]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
+    }
+#ifndef FA2_EXP_NOSYNC
+    vm_wait_all();
+    __syncthreads();
+#endif
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  int i = 0;
+  for (; i + 1 < n_steady; i += 2) {
+    step(i, s, s2, T{}, F{});
+    step(i + 1, s2, s, T{}, F{});
+  }
+  if (i < n_steady) {
+    step(i, s, s2, T{}, F{});
+    s[0] = s2[0];
+    s[1] = s2[1];
+    ++i;
+  }
+
+  // Tail of this wave: next tile on the diagonal / key tail (pipelined, masked), this wave's
+  // last live tile (softmax + PV only), then tiles past its diagonal (DMA + barrier only).
+  for (; i < ntiles && tile_live(i) && tile_live(i + 1); ++i) {
+    step(i, s, s2, T{}, T{});
+    s[0] = s2[0];
+    s[1] = s2[1];
+  }
+  if (i < ntiles && tile_live(i)) {
+    step(i, s, s2, F{}, F{});
+    ++i;
+  }
+  for (; i < ntiles; ++i) {
+#pragma unroll
+    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
+    vm_wait_all();
+    __syncthreads();
+  }
+
+  // ---- epilogue ----------------------------------------------------------------------------
+  const float l_tot = half_sum(l_run);
+  const bool row_ok = qi < Lq && l_tot > 0.f;
+  const float inv = row_ok ? 1.f / l_tot : 0.f;
+  if (hh == 0 && qi < p.lse_row_stride) {
+    float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
+    lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
+  }
+  if (qi < p.seqlen_q) {
+    uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        const float o0 = acc[dt][4 * g4 + 0] * inv, o1 = acc[dt][4 * g4 + 1] * inv;
+        const float o2 = acc[dt][4 * g4 + 2] * inv, o3 = acc[dt][4 * g4 + 3] * inv;
+        if (d0 < D) *(u32x2*)(orow + d0) = u32x2{E::pack2(o0, o1), E::pack2(o2, o3)};
+      }
+    }
+  }
+}
+
+template <bool BF16, int DT, bool CAUSAL>
+static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
+  constexpr int BM = 128;
+  dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace fa2
