@@ -28,10 +28,14 @@ namespace fa2 {
 #define FA2_FWD_PIPE 2
 #endif
 
-template <bool BF16, int DT, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+#ifndef FA2_FWD_PIPE_NW
+#define FA2_FWD_PIPE_NW 4
+#endif
+
+template <bool BF16, int DT, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = 4, NT = NW * 64;
+  constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
   constexpr int KS = DT / 16;        // k-steps of Q K^T
@@ -101,6 +105,7 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
 
   const float sc = p.softmax_scale * kLog2e;
   float m_run = kNegInf, l_run = 0.f;
+  float m_ref = 0.f;  // the max the stored exponent arguments are relative to (0 while m_run = -inf)
   f32x16 acc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
@@ -156,33 +161,42 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
     }
   };
 
-  // defer-max decision for the scores in s; returns m_use, rescales O when the max moved
-  auto softmax_begin = [&]() {
+  // Defer-max decision for the tile whose exponent arguments z = s * sc - m_ref sit in z[].
+  // Usually the running max stays (m_use == m_ref) and z is final; when some row of the wave
+  // outgrew it by more than kDeferMax, O and l are rescaled and z shifted (rare: first tiles).
+  auto softmax_begin = [&](f32x16* z) {
     const bool rescale = !__all(mx - m_run <= kDeferMax);
-    const float m_new = rescale ? fmaxf(m_run, mx) : m_run;
-    const float m_use = m_new == kNegInf ? 0.f : m_new;
     if (rescale) {
+      const float m_new = fmaxf(m_run, mx);
+      const float m_use = m_new == kNegInf ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+      const float shift = m_use - m_ref;
       l_run *= alpha;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) z[t][i] -= shift;
+      m_run = m_new;
+      m_ref = m_use;
     }
-    m_run = m_new;
-    return m_use;
+  };
+  // exponent arguments of the scores in v (in place), relative to the current reference max
+  auto to_z = [&](f32x16* v) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[t][i] = fmaf(v[t][i], sc, -m_ref);
   };
 
   // exponentials e..e+1 of the flat 32-score list -> P, row-sum partials
-  auto exp_pair = [&](const f32x16* src, int e, float m_use, float& rs0, float& rs1) {
+  auto exp_pair = [&](const f32x16* src, int e, float& rs0, float& rs1) {
     const int t = e >> 4, i = e & 15;
-#ifdef FA2_EXP_NOEXP
-    const float p0 = fmaf(src[t][i], sc, -m_use);
-    const float p1 = fmaf(src[t][i + 1], sc, -m_use);
-#else
-    const float p0 = __builtin_amdgcn_exp2f(fmaf(src[t][i], sc, -m_use));
-    const float p1 = __builtin_amdgcn_exp2f(fmaf(src[t][i + 1], sc, -m_use));
-#endif
+    const float p0 = __builtin_amdgcn_exp2f(src[t][i]);
+    const float p1 = __builtin_amdgcn_exp2f(src[t][i + 1]);
     rs0 += p0;
     rs1 += p1;
     pf[t][i >> 3][(i & 7) >> 1] = E::pack2(p0, p1);
@@ -196,6 +210,7 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
     qk_plain(kt(0));
     if (tile_mask(0)) mask_max(0);
     else plain_max();
+    to_z(s);
   }
   __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
 
@@ -234,7 +249,7 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
     // the other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume
     // cur[0] then cur[1]: 48 score registers live at any step, not 64.
     {
-      const float m_use = softmax_begin();
+      softmax_begin(cur);
       float rs0 = 0.f, rs1 = 0.f;
       u32x4 kf[NQK];
       auto kfs = [&](int m) { return kfrag(K1, 2 * (m % KS) + m / KS); };
@@ -250,10 +265,8 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
           nxt[t] = E::mfma(kf[m], qf[ks], ks == 0 ? zero16() : nxt[t]);
         }
 #pragma unroll
-        for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, m_use, rs0, rs1);
-#ifndef FA2_EXP_NODMA
+        for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
         if (m % kEvery == 0 && m / kEvery < 2 * kPieces) dma(i, m / kEvery);
-#endif
         __builtin_amdgcn_sched_barrier(0);
       }
       l_run += rs0 + rs1;
@@ -282,16 +295,15 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
             }
             float& mm = t ? mb_ : ma;
             mm = fmaxf(mm, nxt[t][r]);
+            nxt[t][r] = fmaf(nxt[t][r], sc, -m_ref);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
     }
-#ifndef FA2_EXP_NOSYNC
     vm_wait_all();
     __syncthreads();
-#endif
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -350,9 +362,9 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
 
 template <bool BF16, int DT, bool CAUSAL>
 static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int BM = 128;
+  constexpr int NW = FA2_FWD_PIPE_NW, BM = NW * 32;
   dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, NW>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
 
