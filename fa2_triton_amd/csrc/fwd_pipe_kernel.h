@@ -28,13 +28,20 @@ namespace fa2 {
 #define FA2_FWD_PIPE 2
 #endif
 
-#ifndef FA2_FWD_PIPE_NW
-#define FA2_FWD_PIPE_NW 4
+#ifndef FA2_FWD_PP
+#define FA2_FWD_PP 0  // ping-pong schedule: 0 never, 1 non-causal only, 2 always
 #endif
 
-template <bool BF16, int DT, bool CAUSAL, int NW>
-__global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+template <bool PP>
+struct PipeCfg {
+  static constexpr int NW = PP ? 8 : 4;   // waves per workgroup
+  static constexpr int NKB = PP ? 3 : 2;  // K tile buffers
+};
+
+template <bool BF16, int DT, bool CAUSAL, bool PP>
+__global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
+  constexpr int NW = PipeCfg<PP>::NW, NKB = PipeCfg<PP>::NKB;
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
@@ -45,7 +52,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   constexpr int EPS = 32 / NQK;      // exponentials per QK^T step
   constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
   constexpr int LEAD = 3;            // fragment reads in flight ahead of their MFMA
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // K0 K1 V0 V1
+  __shared__ __attribute__((aligned(16))) char smem[(NKB + 2) * TILE];  // K buffers, V0 V1
   static_assert(NQK % 8 == 0 && 32 % NQK == 0, "QK^T steps must carry whole pack pairs");
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -66,7 +73,10 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     Lq = Lk = p.cu_seqlens[b + 1] - cu;
   }
   const int m0 = mb * BM;
-  const int qw0 = m0 + w * 32;  // first row of this wave
+  // ping-pong: waves w and w + 4 share a SIMD and run in opposite groups g; the groups take
+  // alternate 32-row blocks so that both see the same causal extent
+  const int g = PP ? (w >> 2) : 0;
+  const int qw0 = m0 + 32 * (PP ? 2 * (w & 3) + g : w);  // first row of this wave
   const int qi = qw0 + r32;     // this lane's query row
   const int D = p.head_dim;
 
@@ -83,8 +93,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   const int ntiles = (n_end + BN - 1) / BN;
   const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
 
-  auto kt = [&](int buf) { return smem + buf * TILE; };
-  auto vt = [&](int buf) { return smem + (2 + buf) * TILE; };
+  auto kt = [&](int t) { return smem + (NKB == 2 ? (t & 1) : t % NKB) * TILE; };  // buffer of K tile t
+  auto vt = [&](int t) { return smem + (NKB + (t & 1)) * TILE; };                // buffer of V tile t
   BufStager<DT, BN, NT> kst;  // K and V share row strides (checked by the launcher): one offset set
   kst.init(tid, p.k_stride[1], D);
   const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
@@ -205,29 +215,70 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   __builtin_amdgcn_s_waitcnt(0);  // Q fragments + K0, V0, K1
   __syncthreads();
 
-  // prologue: S(0)
-  if (tile_live(0)) {
-    qk_plain(kt(0));
-    if (tile_mask(0)) mask_max(0);
-    else plain_max();
-    to_z(s);
-  }
-  __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
-
   constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
-  constexpr int kEvery = NQK / (2 * kPieces) > 0 ? NQK / (2 * kPieces) : 1;
+  // DMA pieces per phase: all of K and V in phase X (one barrier per tile), or one tile per
+  // half-phase (ping-pong)
+  constexpr int kPerX = PP ? kPieces : 2 * kPieces;
+  constexpr int kEveryX = NQK / kPerX > 0 ? NQK / kPerX : 1;
+  constexpr int kEveryY = NPV / kPieces > 0 ? NPV / kPieces : 1;
 
-  // DMA targets of iteration i: K(i+2) -> K buffer i&1, V(i+1) -> V buffer (i+1)&1.  Rows
-  // past the end read as zeros (buffer range check); tiles wholly past it land in buffers
+  // Rows past the end read as zeros (buffer range check); tiles wholly past it land in buffers
   // nobody reads again.
+  auto dma_k = [&](int t, int pc) {
+    kst.piece(kt(t), BufStager<DT, BN, NT>::tile_rsrc(kg, p.k_stride[1], t * BN, Lk, mrows), pc);
+  };
+  auto dma_v = [&](int t, int pc) {
+    kst.piece(vt(t), BufStager<DT, BN, NT>::tile_rsrc(vg, p.v_stride[1], t * BN, Lk, mrows), pc);
+  };
+  // One-barrier schedule, iteration i: K(i+2) -> the buffer of K(i), V(i+1) -> that of V(i-1).
   auto dma = [&](int i, int pc) {
-    if (pc < kPieces) {
-      kst.piece(kt(i & 1), BufStager<DT, BN, NT>::tile_rsrc(kg, p.k_stride[1], (i + 2) * BN, Lk, mrows), pc);
-    } else {
-      kst.piece(vt((i + 1) & 1), BufStager<DT, BN, NT>::tile_rsrc(vg, p.v_stride[1], (i + 1) * BN, Lk, mrows),
-                pc - kPieces);
+    if (pc < kPieces) dma_k(i + 2, pc);
+    else dma_v(i + 1, pc - kPieces);
+  };
+  // Ping-pong schedule, half-phase h: K(h/2 + 2) when h is even, V((h + 1)/2) when odd.  K has
+  // three buffers: K(t) is read by group 0 in half-phase 2t-2 and by group 1 in 2t-1, and its
+  // buffer is rewritten (by K(t+3)) in half-phase 2t+2.
+  // (target chosen by scalar selects, not a branch: the pieces ride inside fenced MFMA steps)
+  struct DmaTarget {
+    i32x4 rsrc;
+    char* dst;
+  };
+  auto dma_target = [&](int h) {
+    const bool even = (h & 1) == 0;
+    const int t = even ? h / 2 + 2 : (h + 1) / 2;
+    return DmaTarget{BufStager<DT, BN, NT>::tile_rsrc(even ? kg : vg, p.k_stride[1], t * BN, Lk, mrows),
+                     even ? kt(t) : vt(t)};
+  };
+  auto dma_h = [&](const DmaTarget& d, int pc) { kst.piece(d.dst, d.rsrc, pc); };
+  // end of a half-phase: this wave's DMA of the previous half-phase has landed, then barrier
+  auto half_sync = [&]() {
+    if constexpr (kPieces == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if constexpr (kPieces == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (kPieces == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else vm_wait_all();
+    __syncthreads();
+  };
+
+  // prologue: S(0).  Ping-pong: group 0 computes it alone in half-phase -1, group 1 in
+  // half-phase 0 beside group 0's first phase X.
+  auto prologue_s0 = [&]() {
+    if (tile_live(0)) {
+      qk_plain(kt(0));
+      if (tile_mask(0)) mask_max(0);
+      else plain_max();
+      to_z(s);
     }
   };
+  // (one copy of the S(0) code for both groups: barriers sit in wave-uniform branches)
+  if (PP && g == 1) __syncthreads();  // half-phase -1
+  prologue_s0();
+  if (!PP || g == 0) {
+    __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
+  } else {
+#pragma unroll
+    for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(0), pc);
+    half_sync();  // half-phase 0
+  }
 
   // Steady-state iterations of this wave: tile i live and tile i+1 live and unmasked.  The
   // count differs between the waves of a workgroup (causal diagonal), so each wave runs its own
@@ -243,8 +294,13 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   // QK: tile i+1 is live for this wave; MASK: it needs the causal / key-tail mask.
   auto step = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto mask_c) {
     constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value;
-    const char* K1 = kt((i + 1) & 1);
-    const char* V0 = vt(i & 1);
+    const char* K1 = kt(i + 1);
+    const char* V0 = vt(i);
+    DmaTarget dx{}, dy{};
+    if constexpr (PP) {
+      dx = dma_target(2 * i + g);
+      dy = dma_target(2 * i + 1 + g);
+    }
     // phase X: QK^T(i+1) with softmax(i) and the DMA pieces riding along.  One key half after
     // the other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume
     // cur[0] then cur[1]: 48 score registers live at any step, not 64.
@@ -266,11 +322,15 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
         }
 #pragma unroll
         for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
-        if (m % kEvery == 0 && m / kEvery < 2 * kPieces) dma(i, m / kEvery);
+        if (m % kEveryX == 0 && m / kEveryX < kPerX) {
+          if constexpr (PP) dma_h(dx, m / kEveryX);
+          else dma(i, m / kEveryX);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       l_run += rs0 + rs1;
     }
+    if constexpr (PP) half_sync();
     // phase Y: PV(i) with the row max of S(i+1), one v_max3 per step
     {
       constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
@@ -285,6 +345,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
         if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
         const int kk = m / NDT;
         acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
+        if constexpr (PP) {
+          if (m % kEveryY == 0 && m / kEveryY < kPieces) dma_h(dy, m / kEveryY);
+        }
         if constexpr (QK) {
 #pragma unroll
           for (int e = m * PER; e < (m + 1) * PER; ++e) {
@@ -302,11 +365,18 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
       }
       if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
     }
-    vm_wait_all();
-    __syncthreads();
+    if constexpr (PP) {
+      half_sync();
+    } else {
+      vm_wait_all();
+      __syncthreads();
+    }
   };
   using T = std::true_type;
   using F = std::false_type;
+#ifdef FA2_EXP_PRIO
+  if (PP && g == 1) __builtin_amdgcn_s_setprio(1);
+#endif
   int i = 0;
   for (; i + 1 < n_steady; i += 2) {
     step(i, s, s2, T{}, F{});
@@ -331,11 +401,25 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     ++i;
   }
   for (; i < ntiles; ++i) {
+    if constexpr (PP) {
 #pragma unroll
-    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
+      for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(2 * i + g), pc);
+      half_sync();
+#pragma unroll
+      for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(2 * i + 1 + g), pc);
+      half_sync();
+    } else {
+#pragma unroll
+      for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
+      vm_wait_all();
+      __syncthreads();
+    }
+  }
+  if (PP && g == 0) {  // group 1's last half-phase
     vm_wait_all();
     __syncthreads();
   }
+  vm_wait_all();
 
   // ---- epilogue ----------------------------------------------------------------------------
   const float l_tot = half_sum(l_run);
@@ -345,27 +429,42 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
     lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
   }
-  if (qi < p.seqlen_q) {
+  // O: lane (r32, hh) holds columns 8k + 4hh .. +3 of its row for k = 4 dt + g4.  One
+  // v_permlane32_swap per dword pairs groups k, k+1 so that each lane stores 16 contiguous
+  // bytes (lanes 0-31: columns 8k..8k+7, lanes 32-63: 8k+8..8k+15): 8 dwordx4 stores instead
+  // of 16 dwordx2 (the store tail is issue-bound).
+  {
     uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
+    const bool row_in = qi < p.seqlen_q;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
-        const float o0 = acc[dt][4 * g4 + 0] * inv, o1 = acc[dt][4 * g4 + 1] * inv;
-        const float o2 = acc[dt][4 * g4 + 2] * inv, o3 = acc[dt][4 * g4 + 3] * inv;
-        if (d0 < D) *(u32x2*)(orow + d0) = u32x2{E::pack2(o0, o1), E::pack2(o2, o3)};
+      for (int g4 = 0; g4 < 4; g4 += 2) {
+        uint32_t a0 = E::pack2(acc[dt][4 * g4 + 0] * inv, acc[dt][4 * g4 + 1] * inv);
+        uint32_t a1 = E::pack2(acc[dt][4 * g4 + 2] * inv, acc[dt][4 * g4 + 3] * inv);
+        uint32_t b0 = E::pack2(acc[dt][4 * g4 + 4] * inv, acc[dt][4 * g4 + 5] * inv);
+        uint32_t b1 = E::pack2(acc[dt][4 * g4 + 6] * inv, acc[dt][4 * g4 + 7] * inv);
+        const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+        const int d0 = 32 * dt + 8 * g4 + 8 * hh;
+        if (row_in && d0 < D) *(u32x4*)(orow + d0) = u32x4{r0[0], r1[0], r0[1], r1[1]};
       }
     }
   }
 }
 
+template <bool BF16, int DT, bool CAUSAL, bool PP>
+static hipError_t launch_fwd_pipe_t(const fa2_fwd_args& a, hipStream_t st) {
+  constexpr int NW = PipeCfg<PP>::NW, BM = NW * 32;
+  dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, PP>), grid, dim3(NW * 64), 0, st, a);
+  return hipGetLastError();
+}
+
 template <bool BF16, int DT, bool CAUSAL>
 static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int NW = FA2_FWD_PIPE_NW, BM = NW * 32;
-  dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, NW>), grid, dim3(NW * 64), 0, st, a);
-  return hipGetLastError();
+  constexpr bool PP = FA2_FWD_PP >= 2 || (FA2_FWD_PP == 1 && !CAUSAL);
+  return launch_fwd_pipe_t<BF16, DT, CAUSAL, PP>(a, st);
 }
 
 }  // namespace fa2
