@@ -115,7 +115,8 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   const int D = a->head_dim;
   bool aligned = vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
                  vec_ok(D, a->o, a->o_stride) && vec_ok(D, a->dout, a->do_stride) &&
-                 vec_ok(D, a->dk, a->dk_stride) && vec_ok(D, a->dv, a->dv_stride);
+                 vec_ok(D, a->dk, a->dk_stride) && vec_ok(D, a->dv, a->dv_stride) &&
+                 a->k_stride[1] == a->v_stride[1];  // dq_kernel stages K and V with one offset set
   if (a->dq_dtype == FA2_F32)
     aligned = aligned && aligned16(a->dq) && a->dq_stride[0] % 4 == 0 && a->dq_stride[1] % 4 == 0 && a->dq_stride[2] % 4 == 0;
   else

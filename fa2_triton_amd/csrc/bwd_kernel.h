@@ -29,6 +29,12 @@
 #ifndef FA2_DQ_LEAD
 #define FA2_DQ_LEAD 2
 #endif
+#ifndef FA2_DQ_PIPE
+#define FA2_DQ_PIPE 1  // software-pipelined interior tiles in dq_kernel
+#endif
+#ifndef FA2_DQ_PIPE_LEAD
+#define FA2_DQ_PIPE_LEAD 1
+#endif
 
 namespace fa2 {
 
@@ -125,10 +131,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
   const int total = n_mt * G;  // (q-head, tile) steps
 
-  Stager<DT, BMQ, NT> qst, ost;
+  // buffer-resource LDS-DMA (rows past Lq read as zeros; masked out of every product)
+  BufStager<DT, BMQ, NT> qst, ost;
+  int qrows = 0, orows = 0;
   if (ALIGNED) {
     qst.init(tid, p.q_stride[1], D);
     ost.init(tid, p.do_stride[1], D);
+    qrows = BufStager<DT, BMQ, NT>::max_rows(p.q_stride[1]);
+    orows = BufStager<DT, BMQ, NT>::max_rows(p.do_stride[1]);
   }
   auto stage = [&](int step, int buf) {
     const int g = step / n_mt, mt = step - g * n_mt;
@@ -137,8 +147,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
     if constexpr (ALIGNED) {
-      qst.issue(qt(buf), qg, p.q_stride[1], m, Lq, tid);
-      ost.issue(ot(buf), og, p.do_stride[1], m, Lq, tid);
+      qst.issue(qt(buf), qg, p.q_stride[1], m, Lq, qrows);
+      ost.issue(ot(buf), og, p.do_stride[1], m, Lq, orows);
     } else {
       stage_tile<DT, BMQ, NT, false>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
       stage_tile<DT, BMQ, NT, false>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
@@ -411,15 +421,18 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   const int ntiles = (n_end + BN - 1) / BN;
   auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
   auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
-  Stager<DT, BN, NT> kst, vst;
+  // buffer-resource LDS-DMA, rows past Lk zero-filled; K and V row strides are equal on the
+  // aligned path (api.hip), so one set of lane offsets serves both
+  BufStager<DT, BN, NT> kst;
+  int mrows = 0;
   if (ALIGNED) {
     kst.init(tid, p.k_stride[1], D);
-    vst.init(tid, p.v_stride[1], D);
+    mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
   }
   auto stage_kv = [&](int buf, int n) {
     if constexpr (ALIGNED) {
-      kst.issue(kt(buf), kg, p.k_stride[1], n, Lk, tid);
-      vst.issue(vt(buf), vg, p.v_stride[1], n, Lk, tid);
+      kst.issue(kt(buf), kg, p.k_stride[1], n, Lk, mrows);
+      kst.issue(vt(buf), vg, p.v_stride[1], n, Lk, mrows);
     } else {
       stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, Lk, D, tid);
       stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, Lk, D, tid);
@@ -554,6 +567,70 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     }
   };
 
+  // Interior tiles (no mask, no bias, no dropout): the two 32-key halves are software
+  // pipelined inside the tile so that every softmax-gradient VALU op sits beside an MFMA of
+  // the same wave:
+  //   [S, dP of half 0] [S, dP of half 1 | dS of half 0] [dQ of half 0 | dS of half 1] [dQ of half 1]
+  auto tile_pipe = [&](const char* K, const char* V) {
+    constexpr int L = FA2_DQ_PIPE_LEAD;  // two score pairs live: one step of fragments in flight
+    f32x16 s[2], dp[2];
+    u32x4 dsp[2][2];
+    // dS of element e (0..15) of half t -> packed pair in dsp[t]
+    float dsv_lo = 0.f;
+    auto ds_elem = [&](int t, int e) {
+      const float pr = __builtin_amdgcn_exp2f(fmaf(s[t][e], sc, nlse));
+      const float d = pr * (dp[t][e] - del_i);
+      if (e & 1) dsp[t][e >> 3][(e & 7) >> 1] = E::pack2(dsv_lo, d);
+      else dsv_lo = d;
+    };
+    // S and dP of half t: 2 KS fenced steps; step k of the S/dP chains, VALU hook per step
+    auto sdp = [&](int t, auto hook) {
+      u32x4 fk[KS], fv[KS];
+      auto rd = [&](int ks) {
+        fk[ks] = lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh);
+        fv[ks] = lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh);
+      };
+#pragma unroll
+      for (int j = 0; j < L; ++j) rd(j);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + L < KS) rd(ks + L);
+        s[t] = E::mfma(fk[ks], qf[ks], ks == 0 ? zero16() : s[t]);
+        hook(2 * ks);
+        __builtin_amdgcn_sched_barrier(0);
+        dp[t] = E::mfma(fv[ks], of[ks], ks == 0 ? zero16() : dp[t]);
+        hook(2 * ks + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // dQ^T += K^T dS^T of half t: 2 NDT fenced steps with a VALU hook per step
+    auto dq_half = [&](int t, auto hook) {
+      constexpr int N = 2 * NDT, LL = 2 * L < N ? 2 * L : N;
+      u32x4 fr[N];
+      auto rd = [&](int m) { return lds_tr_frag<DT, BN>(K, 32 * t + 16 * (m / NDT), 32 * (m % NDT), lane); };
+#pragma unroll
+      for (int j = 0; j < LL; ++j) fr[j] = rd(j);
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        if (m + LL < N) fr[m + LL] = rd(m + LL);
+        acc[m % NDT] = E::mfma(fr[m], dsp[t][m / NDT], acc[m % NDT]);
+        hook(m);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    constexpr int SDP_STEPS = 2 * KS, DQ_STEPS = 2 * NDT;
+    sdp(0, [](int) {});
+    sdp(1, [&](int st) {  // 16 dS elements of half 0 over the S/dP steps of half 1
+#pragma unroll
+      for (int e = st * 16 / SDP_STEPS; e < (st + 1) * 16 / SDP_STEPS; ++e) ds_elem(0, e);
+    });
+    dq_half(0, [&](int st) {  // 16 dS elements of half 1 over the dQ steps of half 0
+#pragma unroll
+      for (int e = st * 16 / DQ_STEPS; e < (st + 1) * 16 / DQ_STEPS; ++e) ds_elem(1, e);
+    });
+    dq_half(1, [](int) {});
+  };
+
   for (int it = 0; it < ntiles; ++it) {
     const int cur = it & 1;
     const int n0 = it * BN;
@@ -563,6 +640,8 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     if (!dead) {
       if (need_mask)
         tile(std::true_type{}, kt(cur), vt(cur), n0);
+      else if constexpr (!BIAS && !DROPOUT && FA2_DQ_PIPE)
+        tile_pipe(kt(cur), vt(cur));
       else
         tile(std::false_type{}, kt(cur), vt(cur), n0);
     }

@@ -333,12 +333,14 @@ template <int DT, int ROWS, int NTHREADS>
 struct BufStager {
   static constexpr int kPieces = ROWS * DT / 8;
   static constexpr int kIters = (kPieces + NTHREADS - 1) / NTHREADS;
-  static_assert(kPieces % NTHREADS == 0 && NTHREADS % (ROWS * 4) == 0, "one tile row per lane");
+  static_assert(kPieces % 64 == 0 && (kPieces % NTHREADS == 0 || kIters == 1), "whole wave pieces");
   uint32_t voff[kIters];  // byte offset of this lane's pieces from the tile's first row
   uint32_t wave_lds;      // byte offset of this wave's first piece in the tile (SGPR)
+  int wave;               // wave-uniform (SGPR)
 
   FA2_DEV void init(int tid, int64_t row_stride, int D) {
-    const int wave = tid >> 6, lane = tid & 63, dchunks = D >> 3;
+    wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63, dchunks = D >> 3;
     wave_lds = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
@@ -358,6 +360,7 @@ struct BufStager {
   }
   FA2_DEV static int max_rows(int64_t row_stride) { return (int)min((int64_t)0x7FFFFFFF, 0xFFFFFFFFll / (row_stride * 2)); }
   FA2_DEV void piece(char* tile, i32x4 rsrc, int it) const {
+    if (kPieces % NTHREADS != 0 && wave * 64 >= kPieces) return;  // small tile: idle waves
     const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds + it * NTHREADS * 16;
     uint32_t keep;
     asm volatile(
