@@ -8,8 +8,9 @@ one forward + one backward of that batch.  With N GPUs each rank runs its own B=
 
 FLOPs are algorithmic: fwd = 4 B H S^2 D / 2 (causal), bwd = 2.5 fwd.
 
-Besides the step time, every launch of the path -- forward, and the backward's delta, dK/dV and
-dQ kernels (fa2_bwd_stages) -- is timed with HIP events on the stream it runs on.  `roofline`
+Besides the step time, every launch of the path -- the forward, and the backward's dQ kernel
+(which also computes delta = rowsum(O * dO)) and dK/dV kernel (fa2_bwd_stages) -- is timed with
+HIP events on the stream it runs on.  `roofline`
 is the dominant (longest) kernel, `roofline_fwd` the north-star forward kernel, each with its
 algorithmic FLOPs per launch and the HBM bytes per launch from the committed rocprofv3 PMC
 summary (profiles/*_pmc.json).  Rank 0 also times the CPU oracle (oracle/reference.py, fp32,
@@ -172,19 +173,20 @@ def main():
     value, ms_per_step = job_throughput(f_fwd, args.steps, world, elapsed)
 
     # ---- per-launch timing with HIP events on the launch stream ---------------------------
-    # fwd: one launch; bwd: delta, dK/dV and dQ launches timed separately via fa2_bwd_stages.
+    # fwd: one launch; bwd: the dQ (+ delta) and dK/dV launches timed separately (fa2_bwd_stages).
     reps = max(5, args.steps)
     stream = torch.cuda.current_stream(device)
     with torch.no_grad():
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        # one delta workspace for all timed calls: the dQ launch (first) writes rowsum(O * dO)
+        # into it, the dK/dV launch reads it
+        delta = torch.empty_like(lse)
         calls = {
             "fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
-            "delta_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
-                                                         _stages=1),
-            "dkdv_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
-                                                        _stages=2),
             "dq_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
-                                                      _stages=4),
+                                                      _stages=4, _delta=delta),
+            "dkdv_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
+                                                        _stages=2, _delta=delta),
         }
         times = {}
         for name, fn in calls.items():
@@ -197,14 +199,14 @@ def main():
             torch.cuda.synchronize()
             times[name] = e0.elapsed_time(e1) / reps * 1e-3
     t_fwd = times["fwd_kernel"]
-    t_bwd = times["delta_kernel"] + times["dkdv_kernel"] + times["dq_kernel"]
+    t_bwd = times["dkdv_kernel"] + times["dq_kernel"]
     fwd_tf = f_fwd / t_fwd / 1e12
     bwd_tf = 2.5 * f_fwd / t_bwd / 1e12
     # Algorithmic FLOPs per launch: fwd = F; the backward's 5 GEMM-units
     # (2.5 F) are split as S, dP, dV, dK -> dK/dV kernel (2 F) and dQ -> dQ kernel (0.5 F).
     # The dQ kernel also recomputes S and dP (1 F executed but not algorithmic).
-    algo = {"fwd_kernel": f_fwd, "delta_kernel": 0.0, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd}
-    executed = {"fwd_kernel": f_fwd, "delta_kernel": 0.0, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 1.5 * f_fwd}
+    algo = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd}
+    executed = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 1.5 * f_fwd}
     kernels = {
         name: {
             "ms": round(t * 1e3, 4),
@@ -217,12 +219,15 @@ def main():
     pmc["_workload_ok"] = (b, h, s, d, causal) == (8, 32, 4096, 128, True)
     dominant = max(("fwd_kernel", "dkdv_kernel", "dq_kernel"), key=lambda n: times[n])
 
+    # device symbols the default workload dispatches to (aligned D, no bias, no dropout)
+    symbol = {"fwd_kernel": "fwd_pipe_kernel", "dkdv_kernel": "dkdv_kernel", "dq_kernel": "dq_kernel"}
+
     def roofline(name):
         ach = algo[name] / times[name] / 1e12
-        traffic = pmc.get(name, {}).get("hbm_bytes_per_launch") if pmc.get("_workload_ok") else None
+        traffic = pmc.get(symbol[name], {}).get("hbm_bytes_per_launch") if pmc.get("_workload_ok") else None
         return {
             "bound": "mfma",
-            "kernel": f"fa2::{name}",
+            "kernel": f"fa2::{symbol[name]}",
             "achieved": round(ach, 2),
             "peak": PEAK_TFLOPS,
             "unit": "TFLOP/s",

@@ -34,7 +34,8 @@ def _flash_attn_backward(
     softmax_scale: Optional[float],
     dropout_seed: Optional[int],
     dq_dtype: Optional[torch.dtype] = None,
-    _stages: int = 7,
+    _stages: int = 6,
+    _delta: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, Tensor]:
     if attention_mask is not None:
         assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
@@ -57,7 +58,7 @@ def _flash_attn_backward(
     dq = torch.empty(q.shape, dtype=dq_dtype, device=q.device)
     dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
     dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
-    delta = torch.empty_like(lse)
+    delta = torch.empty_like(lse) if _delta is None else _delta  # workspace: rowsum(O * dO)
 
     args = _lib.BwdArgs()
     args.q, args.k, args.v, args.o, args.dout = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr()

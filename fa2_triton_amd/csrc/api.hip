@@ -138,7 +138,7 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   return hip_status(e, "fa2_bwd launch");
 }
 
-int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, 7, stream); }
+int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, 6, stream); }
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,
                              int32_t* cu_seqlens, void* stream) {

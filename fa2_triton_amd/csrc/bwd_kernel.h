@@ -1,7 +1,8 @@
 // bwd.hip -- FlashAttention-2 backward for gfx950 (CDNA4).
 //
 // Replaces the reference's backward launches (/root/reference/src/backward/caller.py:95-165):
-//   delta_kernel  <- _compute_delta        (/root/reference/src/backward/compute_delta.py:17-73)
+//   delta_kernel  <- _compute_delta        (/root/reference/src/backward/compute_delta.py:17-73);
+//                    the default backward folds it into dq_kernel, which runs first
 //   dkdv_kernel   <- _bwd_kernel, pid < NUM_BLOCKS_KV branch + the host GQA sum
 //                    (/root/reference/src/backward/kernel.py:154-166, compute_dkdv.py:7-296,
 //                     caller.py:162-165)
@@ -453,7 +454,25 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   }
   const int64_t srow = (int64_t)bh * p.lse_row_stride;
   const float lse_i = qvalid ? p.lse[srow + qi] : 0.f;
-  const float del_i = qvalid ? p.delta[srow + qi] : 0.f;
+  // delta_i = rowsum(O * dO) of this lane's row (/root/reference/src/backward/compute_delta.py:
+  // 17-73), computed here from the dO fragments already in registers and published to the
+  // workspace for dkdv_kernel, which runs after this kernel (rows [Lq, grid rows) get 0)
+  float del_i;
+  {
+    const uint16_t* orow = (const uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)(qvalid ? qi : 0) * p.o_stride[1];
+    float part = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const u32x4 ov = load_row_frag<ALIGNED>(orow, 16 * ks + 8 * hh, D, qvalid);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        part = fmaf(E::to_f32((uint16_t)(ov[j] & 0xFFFF)), E::to_f32((uint16_t)(of[ks][j] & 0xFFFF)), part);
+        part = fmaf(E::to_f32((uint16_t)(ov[j] >> 16)), E::to_f32((uint16_t)(of[ks][j] >> 16)), part);
+      }
+    }
+    del_i = qvalid ? half_sum(part) : 0.f;
+    if (hh == 0 && qi < p.lse_row_stride) p.delta[srow + qi] = del_i;
+  }
 
   f32x16 acc[NDT];
 #pragma unroll
@@ -687,13 +706,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 // ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
+  // order: standalone delta (bit 0), dQ (bit 2; also writes delta), then dK/dV (bit 1, reads it)
   if (stages & 1) {
     dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
-  }
-  if (stages & 2) {
-    dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if (stages & 4) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
@@ -702,6 +718,10 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
     else
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
+  }
+  if (stages & 2) {
+    dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }

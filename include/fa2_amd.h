@@ -109,9 +109,11 @@ typedef struct fa2_bwd_args {
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
 int fa2_bwd(const fa2_bwd_args* args, void* stream);
 
-/* fa2_bwd restricted to some of its three launches (bit 0: delta = rowsum(O * dO), bit 1:
- * dK/dV, bit 2: dQ; each later stage needs the earlier ones' outputs) -- for per-kernel timing
- * and profiling; fa2_bwd == fa2_bwd_stages(args, 7, stream). */
+/* The backward's launches selected by a bit mask, for per-kernel timing and profiling.
+ * Launch order: bit 0 delta = rowsum(O * dO) (standalone kernel), bit 2 dQ (which also computes
+ * delta for its rows and writes it to args->delta), bit 1 dK/dV (reads delta).  A mask must
+ * produce delta before dK/dV reads it (bit 0 or bit 2, now or in an earlier call);
+ * fa2_bwd == fa2_bwd_stages(args, 6, stream). */
 int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
 
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,

@@ -33,16 +33,19 @@ k = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 v = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 do = torch.randn_like(q)
 F = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
-flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F}
+flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F, "bwd": 3.5 * F}
 results = {(n, w): [] for n, _ in libs for w in what}
 for rnd in range(5):
     for name, lib in libs:
         L._lib = lib
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        delta = torch.empty_like(lse)
+        _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=1, _delta=delta)
         calls = {
             "fwd": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
-            "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=3),
-            "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=5),
+            "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=2, _delta=delta),
+            "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=4, _delta=delta),
+            "bwd": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None),
         }
         for w in what:
             calls[w]()
