@@ -8,9 +8,10 @@ one forward + one backward of that batch.  With N GPUs each rank runs its own B=
 
 FLOPs are algorithmic: fwd = 4 B H S^2 D / 2 (causal), bwd = 2.5 fwd.
 
-Besides the step time, every launch of the path -- the forward, and the backward's dQ kernel
-(which also computes delta = rowsum(O * dO)) and dK/dV kernel (fa2_bwd_stages) -- is timed with
-HIP events on the stream it runs on.  `roofline`
+Besides the step time, every launch of the path -- the forward, and the backward's delta,
+dK/dV (+ dS tiles) and dQ = dS K kernels (fa2_bwd_stages; without the dS workspace: the
+recompute dQ kernel, which also computes delta, and dK/dV) -- is timed with HIP events on the
+stream it runs on.  `roofline`
 is the dominant (longest) kernel, `roofline_fwd` the north-star forward kernel, each with its
 algorithmic FLOPs per launch and the HBM bytes per launch from the committed rocprofv3 PMC
 summary (profiles/*_pmc.json).  Rank 0 also times the CPU oracle (oracle/reference.py, fp32,
@@ -29,6 +30,7 @@ import time
 import torch
 
 PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md: ~8 TB/s)
 METRIC = "attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16; % of MFMA peak"
 
 
@@ -137,7 +139,7 @@ def main():
     device = torch.device("cuda", local_rank)
 
     from fa2_triton_amd import flash_attn_func
-    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.backward import _flash_attn_backward, alloc_ds_workspace
     from fa2_triton_amd.forward import _flash_attn_forward
 
     # weak scaling: the global batch is --batch per GPU; this rank owns rows [lo, hi) of it
@@ -173,21 +175,25 @@ def main():
     value, ms_per_step = job_throughput(f_fwd, args.steps, world, elapsed)
 
     # ---- per-launch timing with HIP events on the launch stream ---------------------------
-    # fwd: one launch; bwd: the dQ (+ delta) and dK/dV launches timed separately (fa2_bwd_stages).
+    # fwd: one launch; bwd: its launches timed one by one (fa2_bwd_stages).  With the dS
+    # workspace (the default at this size): delta, dK/dV (+ dS tiles), dQ = dS K; without it:
+    # dQ (recomputes S, dP; also writes delta), then dK/dV.
     reps = max(5, args.steps)
     stream = torch.cuda.current_stream(device)
     with torch.no_grad():
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
-        # one delta workspace for all timed calls: the dQ launch (first) writes rowsum(O * dO)
-        # into it, the dK/dV launch reads it
-        delta = torch.empty_like(lse)
-        calls = {
-            "fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
-            "dq_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
-                                                      _stages=4, _delta=delta),
-            "dkdv_kernel": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
-                                                        _stages=2, _delta=delta),
-        }
+        delta = torch.empty_like(lse)  # shared by the stage calls: written first, read by dK/dV
+        ws = alloc_ds_workspace(q, k)  # shared too: dK/dV writes the dS tiles dQ reads
+
+        def bwd(stages):
+            return lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None,
+                                                _stages=stages, _delta=delta, _ds_ws=ws, _use_ds=ws is not None)
+
+        calls = {"fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)}
+        if ws is not None:
+            calls.update(delta_kernel=bwd(1), dkdv_kernel=bwd(2), dq_kernel=bwd(4))
+        else:
+            calls.update(dq_kernel=bwd(4), dkdv_kernel=bwd(2))
         times = {}
         for name, fn in calls.items():
             fn()
@@ -198,15 +204,23 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             times[name] = e0.elapsed_time(e1) / reps * 1e-3
+        del ws
     t_fwd = times["fwd_kernel"]
-    t_bwd = times["dkdv_kernel"] + times["dq_kernel"]
+    t_bwd = sum(t for n, t in times.items() if n != "fwd_kernel")
     fwd_tf = f_fwd / t_fwd / 1e12
     bwd_tf = 2.5 * f_fwd / t_bwd / 1e12
     # Algorithmic FLOPs per launch: fwd = F; the backward's 5 GEMM-units
     # (2.5 F) are split as S, dP, dV, dK -> dK/dV kernel (2 F) and dQ -> dQ kernel (0.5 F).
-    # The dQ kernel also recomputes S and dP (1 F executed but not algorithmic).
-    algo = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd}
-    executed = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 1.5 * f_fwd}
+    # The recompute dQ kernel also recomputes S and dP (1 F executed but not algorithmic); the
+    # dS-path dQ kernel executes exactly its 0.5 F, and is bound by HBM (the dS stream).
+    ds_path = "delta_kernel" in times
+    algo = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd, "delta_kernel": 0.0}
+    executed = dict(algo, dq_kernel=(0.5 if ds_path else 1.5) * f_fwd)
+    # HBM bytes the dS-path dQ kernel must move: the dS tiles it reads (2 KiB per visited
+    # 32 x 32 (query, key) tile) + K once + dQ written
+    nt = -(-s // 32)
+    tiles = nt * (nt + 1) // 2 if causal else nt * nt
+    dq_bytes = b * h * tiles * 2048 + b * s * h * d * 2 * 2
     kernels = {
         name: {
             "ms": round(t * 1e3, 4),
@@ -215,16 +229,24 @@ def main():
         }
         for name, t in times.items()
     }
+    if ds_path:
+        kernels["dq_kernel"]["hbm_gbps"] = round(dq_bytes / times["dq_kernel"] / 1e9, 1)
     pmc = load_pmc()
     pmc["_workload_ok"] = (b, h, s, d, causal) == (8, 32, 4096, 128, True)
     dominant = max(("fwd_kernel", "dkdv_kernel", "dq_kernel"), key=lambda n: times[n])
 
     # device symbols the default workload dispatches to (aligned D, no bias, no dropout)
-    symbol = {"fwd_kernel": "fwd_pipe_kernel", "dkdv_kernel": "dkdv_kernel", "dq_kernel": "dq_kernel"}
+    symbol = {"fwd_kernel": "fwd_pipe_kernel", "dkdv_kernel": "dkdv_kernel", "delta_kernel": "delta_kernel",
+              "dq_kernel": "dq_ds_kernel" if ds_path else "dq_kernel"}
 
     def roofline(name):
-        ach = algo[name] / times[name] / 1e12
         traffic = pmc.get(symbol[name], {}).get("hbm_bytes_per_launch") if pmc.get("_workload_ok") else None
+        if name == "dq_kernel" and ds_path:
+            ach = dq_bytes / times[name] / 1e9
+            return {"bound": "hbm", "kernel": f"fa2::{symbol[name]}", "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS,
+                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": dq_bytes}
+        ach = algo[name] / times[name] / 1e12
         return {
             "bound": "mfma",
             "kernel": f"fa2::{symbol[name]}",
@@ -274,6 +296,8 @@ def main():
         "pct_of_peak_fwd_bwd": round(100 * value / world / PEAK_TFLOPS, 2),
         "roofline": roofline(dominant),
         "roofline_fwd": roofline("fwd_kernel"),
+        "roofline_dq": roofline("dq_kernel"),
+        "bwd_path": "dS workspace (delta, dK/dV + dS tiles, dQ = dS K)" if ds_path else "recompute dQ",
         "kernels": kernels,
         "cpu_baseline": cpu,
     }

@@ -94,11 +94,15 @@ class BwdArgs(ctypes.Structure):
         ("softmax_scale", ctypes.c_float),
         ("dropout_p", ctypes.c_float),
         ("dropout_seed", ctypes.c_uint64),
+        ("ds_workspace", ctypes.c_void_p),
+        ("ds_workspace_bytes", ctypes.c_int64),
     ]
 
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_cu_seqlens_from_mask", "fa2_last_error",
-                    "fa2_version")
+ABI_VERSION = 2  # FA2_ABI_VERSION in include/fa2_amd.h
+
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_ds_workspace_bytes", "fa2_cu_seqlens_from_mask",
+                    "fa2_last_error", "fa2_version")
 
 _lock = threading.Lock()
 _lib = None
@@ -124,6 +128,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_bwd.restype = ctypes.c_int
         lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.c_void_p]
         lib.fa2_bwd_stages.restype = ctypes.c_int
+        lib.fa2_bwd_ds_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
+        lib.fa2_bwd_ds_workspace_bytes.restype = ctypes.c_int64
         lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
         lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int
@@ -132,8 +138,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_version.argtypes = []
         lib.fa2_version.restype = ctypes.c_int
         version = lib.fa2_version()
-        if version != 1:
-            raise RuntimeError(f"fa2_triton_amd: library ABI version {version}, expected 1")
+        if version != ABI_VERSION:
+            raise RuntimeError(f"fa2_triton_amd: library ABI version {version}, expected {ABI_VERSION}")
         _lib = lib
     return _lib
 

@@ -11,6 +11,7 @@ unpack, :29-79, :167-176).
 """
 import ctypes
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -18,6 +19,36 @@ from torch import Tensor
 
 from . import _lib
 from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, stream_of
+
+
+def ds_workspace_bytes(q: Tensor, k: Tensor) -> int:
+    """Bytes of the dS workspace (`fa2_bwd_ds_workspace_bytes`): one 2 KiB tile of rounded
+    dS per (batch, q-head, 32-query tile, 32-key tile); 0 where the path does not apply
+    (head_dim not a multiple of 8, <= 32 or > 128)."""
+    batch, seqlen_q, nheads_q, head_dim = q.shape
+    seqlen_k = k.shape[1]
+    if head_dim % 8 != 0 or head_dim <= 32 or head_dim > 128 or seqlen_q == 0 or seqlen_k == 0:
+        return 0
+    return batch * nheads_q * math.ceil(seqlen_q / 32) * math.ceil(seqlen_k / 32) * 2048
+
+
+def _ds_workspace_cap(device: torch.device) -> int:
+    """Largest dS workspace the backward allocates by itself: FA2_DS_WORKSPACE_MAX_GB (0
+    disables the dS path), default a quarter of the device's memory (72 GB of a 288 GB MI355X;
+    B=8 H=32 S=4096 needs 8.6 GB)."""
+    env = os.environ.get("FA2_DS_WORKSPACE_MAX_GB")
+    if env is not None:
+        return int(float(env) * (1 << 30))
+    return torch.cuda.get_device_properties(device).total_memory // 4
+
+
+def alloc_ds_workspace(q: Tensor, k: Tensor) -> Optional[Tensor]:
+    """The dS workspace for a backward of these shapes, or None when the dS path does not apply
+    or would exceed the cap (the backward then recomputes S and dP in its dQ kernel)."""
+    nbytes = ds_workspace_bytes(q, k)
+    if nbytes == 0 or nbytes > _ds_workspace_cap(q.device):
+        return None
+    return torch.empty(nbytes, dtype=torch.uint8, device=q.device)
 
 
 def _flash_attn_backward(
@@ -34,8 +65,10 @@ def _flash_attn_backward(
     softmax_scale: Optional[float],
     dropout_seed: Optional[int],
     dq_dtype: Optional[torch.dtype] = None,
-    _stages: int = 6,
+    _stages: Optional[int] = None,
     _delta: Optional[Tensor] = None,
+    _ds_ws: Optional[Tensor] = None,
+    _use_ds: Optional[bool] = None,
 ) -> Tuple[Tensor, Tensor, Tensor]:
     if attention_mask is not None:
         assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
@@ -85,7 +118,16 @@ def _flash_attn_backward(
     args.softmax_scale = float(softmax_scale)
     args.dropout_p = float(dropout_p)
     args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
+    # dS workspace: dK/dV stores its rounded dS tiles and dQ = dS K streams them (one GEMM)
+    # instead of recomputing S and dP; the caller may pass one (stage-by-stage timing)
+    if _use_ds is False:
+        ds_ws = None
+    else:
+        ds_ws = _ds_ws if _ds_ws is not None else alloc_ds_workspace(q, k)
+    if ds_ws is not None:
+        args.ds_workspace, args.ds_workspace_bytes = ds_ws.data_ptr(), ds_ws.numel() * ds_ws.element_size()
+    stages = _stages if _stages is not None else (7 if ds_ws is not None else 6)
     lib = _lib.load()
     with torch.cuda.device(q.device):
-        _lib.check(lib.fa2_bwd_stages(ctypes.byref(args), _stages, stream_of(q)))
+        _lib.check(lib.fa2_bwd_stages(ctypes.byref(args), stages, stream_of(q)))
     return dq, dk, dv

@@ -121,6 +121,13 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
     aligned = aligned && aligned16(a->dq) && a->dq_stride[0] % 4 == 0 && a->dq_stride[1] % 4 == 0 && a->dq_stride[2] % 4 == 0;
   else
     aligned = aligned && vec_ok(D, a->dq, a->dq_stride);
+  if (a->ds_workspace) {
+    const int64_t need = fa2_bwd_ds_workspace_bytes(a);
+    if (need == 0) return fail(FA2_E_INVALID, "ds_workspace given but the dS path does not apply (head_dim %d)", D);
+    if (a->ds_workspace_bytes < need)
+      return fail(FA2_E_INVALID, "ds_workspace_bytes %lld < %lld required", (long long)a->ds_workspace_bytes, (long long)need);
+    if (!aligned16(a->ds_workspace)) return fail(FA2_E_INVALID, "ds_workspace must be 16-byte aligned");
+  }
   hipStream_t st = (hipStream_t)stream;
   const bool bf = a->dtype == FA2_BF16;
   const int dt = pick_dt(D);
@@ -138,7 +145,14 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   return hip_status(e, "fa2_bwd launch");
 }
 
-int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, 6, stream); }
+int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, a && a->ds_workspace ? 7 : 6, stream); }
+
+int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* a) {
+  // head dims 40..128 (multiples of 8): the 3-buffer dq_ds_kernel ring of D = 256 tiles would not fit in LDS
+  if (!a || a->head_dim % 8 != 0 || a->head_dim <= 32 || a->head_dim > 128 || a->batch < 1 || a->heads_q < 1) return 0;
+  if (a->seqlen_q <= 0 || a->seqlen_k <= 0) return 0;
+  return (int64_t)a->batch * a->heads_q * ((a->seqlen_q + 31) / 32) * ((a->seqlen_k + 31) / 32) * (32 * 32 * 2);
+}
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,
                              int32_t* cu_seqlens, void* stream) {

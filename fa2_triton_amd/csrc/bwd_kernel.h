@@ -24,8 +24,26 @@
 #ifndef FA2_DKDV_LEAD
 #define FA2_DKDV_LEAD 1
 #endif
+#ifndef FA2_DKDV_SEQ
+#define FA2_DKDV_SEQ 1  // S chain then dP chain with deeper fragment prefetch
+#endif
+#ifndef FA2_DKDV_LS
+#define FA2_DKDV_LS 2  // S-chain fragments in flight (MFMAs ahead)
+#endif
+#ifndef FA2_DKDV_LD
+#define FA2_DKDV_LD 1  // dP-chain fragment pairs in flight
+#endif
 #ifndef FA2_DKDV_ABL
 #define FA2_DKDV_ABL 0  // timing ablations of dK/dV: 1 = no P/dS VALU, 2 = no Q/dO prefetch
+#endif
+#ifndef FA2_DS_ST_NT
+#define FA2_DS_ST_NT 1  // dS workspace stores non-temporal (measured 1.5 % faster dK/dV)
+#endif
+#ifndef FA2_DS_ABL
+#define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs
+#endif
+#ifndef FA2_DS_LD_POLICY
+#define FA2_DS_LD_POLICY "nt "  // cache policy of the dS workspace loads (once-read stream)
 #endif
 #ifndef FA2_DQ_LEAD
 #define FA2_DQ_LEAD 2
@@ -38,6 +56,10 @@
 #endif
 
 namespace fa2 {
+
+constexpr int kDsChunk = 32 * 32 * 2;  // bytes of one 32-key x 32-query dS tile in the workspace
+constexpr int kDqDsWaves = 8;          // dq_ds_kernel: waves (32 query rows each) per workgroup
+constexpr int kDqDsStages = 3;         // dq_ds_kernel: K + dS tiles in LDS (two in flight)
 
 // ---------------------------------------------------------------------------------------------
 // delta[b, h, i] = sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows)
@@ -84,7 +106,7 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 //   dK^T[d][key] += Q^T dS  NDT*2 MFMA
 // dK/dV accumulate the whole GQA group in fp32 and are rounded once.  <= 256 VGPRs, so two
 // workgroups share a CU (DT <= 128).
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED, bool DSOUT>
 __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NT = 256;
@@ -182,7 +204,38 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
-#if FA2_DKDV_LEAD
+#if FA2_DKDV_SEQ
+    {
+      // fenced steps: the S chain (one fragment per MFMA, read 3 MFMAs ahead), then the dP
+      // chain (two fragments per MFMA, read 2 ahead): deeper prefetch than alternating chains
+      // for the same registers in flight
+      constexpr int LS = FA2_DKDV_LS < KS ? FA2_DKDV_LS : KS, LD = FA2_DKDV_LD < KS ? FA2_DKDV_LD : KS;
+      u32x4 fq[KS], fo[KS], fv[KS];
+#pragma unroll
+      for (int j = 0; j < LS; ++j) fq[j] = lds_row_frag<DT, BMQ>(Q, 0, r32, j, hh);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + LS < KS) fq[ks + LS] = lds_row_frag<DT, BMQ>(Q, 0, r32, ks + LS, hh);
+        // the dP chain's first fragments ride in the S chain's last steps
+        if (ks + LD >= KS) {
+          const int j = ks + LD - KS;
+          fo[j] = lds_row_frag<DT, BMQ>(O, 0, r32, j, hh);
+          fv[j] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, j, hh);
+        }
+        s = E::mfma(fq[ks], kf[ks], s);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + LD < KS) {
+          fo[ks + LD] = lds_row_frag<DT, BMQ>(O, 0, r32, ks + LD, hh);
+          fv[ks + LD] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks + LD, hh);
+        }
+        dp = E::mfma(fo[ks], fv[ks], dp);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#elif FA2_DKDV_LEAD
     {
       // fenced steps, S and dP chains alternating, fragments read FA2_DKDV_LEAD k-steps ahead
       constexpr int L = FA2_DKDV_LEAD < KS ? FA2_DKDV_LEAD : KS;
@@ -269,6 +322,25 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
+    if constexpr (DSOUT) {
+      // publish the rounded dS tile for dq_ds_kernel: chunk (b, hq, q-tile m/32, key block
+      // kw0/32) = 32 key rows of 64 bytes; row kj holds this lane pair's registers as they are
+      // (bytes 32 hh + 16 sp: dsp[sp] = queries 16 sp + 8 (t >> 2) + 4 hh + (t & 3), t = 0..7),
+      // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
+      // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
+      // made dq_ds_kernel's gather 10 % slower.)
+      const int64_t chunk = ((int64_t)(b * p.heads_q + hq) * ((p.seqlen_q + 31) >> 5) + (m >> 5)) *
+                                ((p.seqlen_k + 31) >> 5) + (kw0 >> 5);
+      char* dst = (char*)p.ds_workspace + chunk * kDsChunk + r32 * 64 + 32 * hh;
+#pragma unroll
+      for (int sp = 0; sp < 2 && !(FA2_DS_ABL & 1); ++sp) {
+#if FA2_DS_ST_NT
+        __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
+#else
+        *(u32x4*)(dst + 16 * sp) = dsp[sp];
+#endif
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
 #if FA2_DKDV_LEAD
     {
@@ -334,8 +406,18 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       else
         body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
     }
-    vm_wait_all();
-    __syncthreads();
+    if constexpr (DSOUT) {
+      // the 2 dS stores of this step were issued after the next tile's LDS-DMA: wait for all
+      // but them (vmcnt retires in issue order) and use a raw barrier, whose __syncthreads()
+      // form would drain the stores too; they complete under the next step
+      if ((FA2_DS_ABL & 1) || __builtin_amdgcn_readfirstlane(dead))
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      vm_wait_all();
+      __syncthreads();
+    }
   }
 
   // ---- store dK, dV (kv heads; fp32 group sum rounded once) ----------------------------
@@ -704,8 +786,182 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 }
 
 // ---------------------------------------------------------------------------------------------
+// dQ from stored dS (the dS-workspace path): dQ = scale * dS K, with dS the rounded tiles that
+// dkdv_kernel<..., DSOUT> published.  The same product as dq_kernel's last GEMM
+// (/root/reference/src/backward/compute_dq.py:70-76), without its recompute of S = Q K^T and
+// dP = dO V^T: the pass streams 2 bytes of dS per (query, key) pair from HBM and runs one GEMM
+// instead of three.  One workgroup = 8 waves = 256 query rows of one (batch, q-head); per 64-key
+// tile the K rows (shared by the 8 waves) and each wave's two dS chunks are LDS-DMA'd into a
+// ring of 3 buffers, two tiles in flight (counted vmcnt, raw barriers).
+//   dQ^T[d][q] += K^T dS^T   A = K^T (ds_read_b64_tr_b16 of the K tile),
+//                            B = dS^T (ds_read_b64_tr_b16 of the [key][q] chunk image)
+// A wave reads the chunk of key block j iff dkdv_kernel wrote it: 32 j < Lk and, causal,
+// 32 j <= (first row of the wave) + 31 + (Lk - Lq) -- the complement of dkdv_kernel's `dead`.
+template <bool BF16, int DT, bool CAUSAL, bool DQF32>
+__global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd_args p) {
+  using E = Elem<BF16>;
+  constexpr int NW = kDqDsWaves, NT = NW * 64;
+  constexpr int BM = NW * 32, BN = 64;
+  constexpr int NDT = DT / 32;
+  constexpr int NBUF = kDqDsStages;
+  constexpr int KTILE = BN * DT * 2;        // K tile bytes
+  constexpr int DSW = 2 * kDsChunk;         // one wave's dS image of a tile: 64 keys x 32 queries
+  constexpr int BUF = KTILE + NW * DSW;
+  constexpr int KP = BufStager<DT, BN, NT>::kIters;  // K pieces per lane and tile
+  static_assert(BufStager<DT, BN, NT>::kPieces % NT == 0, "every lane issues the same K pieces");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5;
+  const int nmb = (p.seqlen_q + BM - 1) / BM;
+  const int item = xcd_item(blockIdx.x, gridDim.x);
+  const int bh = item / nmb;
+  const int mbi = item - bh * nmb;
+  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;  // heaviest blocks first
+  const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
+  const int hkv = hq / (p.heads_q / p.heads_kv);
+  int Lq = p.seqlen_q, Lk = p.seqlen_k;
+  if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+  const int D = p.head_dim;
+  const int diag = Lk - Lq;
+  const int m0 = mb * BM;
+  const int mw0 = m0 + 32 * w;
+  // column c = 16 hh + 8 sp + t of a dS chunk row is query 16 sp + 8 (t >> 2) + 4 hh + (t & 3)
+  // of the tile (dkdv_kernel stores its registers as they are): the accumulator column of this
+  // lane is that query
+  const int c = lane & 31;
+  const int qi = mw0 + 16 * ((c >> 3) & 1) + 8 * ((c & 7) >> 2) + 4 * (c >> 4) + (c & 3);
+
+  int n_end = 0;  // keys any row of the workgroup sees
+  if (m0 < Lq) n_end = max(CAUSAL ? min(Lk, m0 + BM + diag) : Lk, 0);
+  int nw_end = 0;  // keys any row of this wave sees: chunk j was written iff 32 j < nw_end
+  if (mw0 < Lq) nw_end = max(CAUSAL ? min(Lk, mw0 + 32 + diag) : Lk, 0);
+  const int ntiles = (n_end + BN - 1) / BN;
+
+  const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
+  auto ktile = [&](int buf) { return smem + buf * BUF; };
+  auto dtile = [&](int buf) { return smem + buf * BUF + KTILE + w * DSW; };
+  BufStager<DT, BN, NT> kst;
+  kst.init(tid, p.k_stride[1], D);
+  const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
+  // this wave's chunk row: chunks (b, hq, q-tile mw0/32, 0 .. nkt) are contiguous; the range
+  // ends at the wave's last written chunk, so the DMA of a chunk past it reads zeros and
+  // every lane issues the same number of pieces per tile (counted vmcnt below)
+  const int nkt = (p.seqlen_k + 31) >> 5;
+  const int64_t crow = ((int64_t)bh * ((p.seqlen_q + 31) >> 5) + (mw0 >> 5)) * nkt;
+  const i32x4 drs = make_rsrc((const char*)p.ds_workspace + crow * kDsChunk,
+                              (uint32_t)min(nkt, (nw_end + 31) >> 5) * kDsChunk);
+  // piece it (0..3) of this lane: 16 bytes of the 4 KB image of two chunks; the image is a
+  // Tile<32, 64> ([64 keys][32 query columns], swizzled 16-byte chunks), the source row-major
+  uint32_t doff[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int pc = it * 64 + lane;
+    const int pr = pc >> 2;                          // key row 0..63 of the image
+    const int cc = (pc & 3) ^ ((pr >> 2) & 3);       // 16-byte column chunk stored at this position
+    doff[it] = (uint32_t)(pr * 64 + cc * 16);        // chunk (pr >> 5) starts at 32 * 64 bytes
+  }
+  auto stage = [&](int buf, int n) {  // KP + 4 VMEM ops per lane
+    kst.issue(ktile(buf), kg, p.k_stride[1], n, Lk, mrows);
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(dtile(buf)));
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(n >> 5) * kDsChunk);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen " FA2_DS_LD_POLICY "lds\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(doff[it]), "s"(drs), "s"(lds + it * 1024), "s"(soff)
+          : "memory");
+    }
+  };
+  constexpr int VM = KP + 4;  // VMEM ops per lane and stage: vmcnt(VM) leaves one stage in flight
+  static_assert(NBUF == 3, "the ring below keeps two stages in flight");
+  if (ntiles > 0) stage(0, 0);
+  if (ntiles > 1) stage(1, BN);
+
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
+  // raw barriers with counted waits: __syncthreads() would drain the tiles in flight
+  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  int cur = 0;
+  for (int it = 0; it < ntiles; ++it) {
+    const int n0 = it * BN;
+    // tile it + 2 goes into the buffer tile it - 1 used (every wave is past its last read)
+    const int nxt2 = cur == 0 ? 2 : cur - 1;
+    if (it + 2 < ntiles) stage(nxt2, n0 + 2 * BN);
+    const char* K = ktile(cur);
+    const char* T = dtile(cur);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if ((FA2_DS_ABL & 2) || n0 + 32 * t >= nw_end) break;  // wave-uniform: chunk not written
+      constexpr int N = 2 * NDT;
+      u32x4 fb[2], fa[N];
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) fb[sp] = lds_tr_frag<32, BN>(T, 32 * t + 16 * sp, 0, lane);
+#pragma unroll
+      for (int m = 0; m < N; ++m) fa[m] = lds_tr_frag<DT, BN>(K, 32 * t + 16 * (m / NDT), 32 * (m % NDT), lane);
+#pragma unroll
+      for (int m = 0; m < N; ++m) acc[m % NDT] = E::mfma(fa[m], fb[m / NDT], acc[m % NDT]);
+    }
+    // tile it + 1 must have landed; tile it + 2 may stay in flight
+    if (it + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    cur = cur == NBUF - 1 ? 0 : cur + 1;
+  }
+
+  if (qi < p.seqlen_q) {
+    const bool ok = qi < Lq;
+    const float scale = p.softmax_scale;
+    char* row = (char*)p.dq + (int64_t)(DQF32 ? 4 : 2) * (b * p.dq_stride[0] + hq * p.dq_stride[2] + (int64_t)qi * p.dq_stride[1]);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        float a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = ok ? acc[dt][4 * g4 + j] * scale : 0.f;
+        if (d0 < D) {
+          if (DQF32)
+            *(f32x4*)((float*)row + d0) = f32x4{a[0], a[1], a[2], a[3]};
+          else
+            *(u32x2*)((uint16_t*)row + d0) = u32x2{E::pack2(a[0], a[1]), E::pack2(a[2], a[3])};
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
+  if constexpr (ALIGNED && (DT == 64 || DT == 128)) {
+    if (a.ds_workspace) {
+      // dS path: delta (bit 0), dK/dV + dS tiles (bit 1), dQ = dS K (bit 2)
+      if (stages & 1) {
+        dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
+        hipLaunchKernelGGL((delta_kernel<BF16, true>), grid, dim3(256), 0, st, a);
+      }
+      if (stages & 2) {
+        dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
+        hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a);
+      }
+      if (stages & 4) {
+        constexpr int BM = kDqDsWaves * 32;
+        dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+        if (a.dq_dtype == FA2_F32)
+          hipLaunchKernelGGL((dq_ds_kernel<BF16, DT, CAUSAL, true>), grid, dim3(kDqDsWaves * 64), 0, st, a);
+        else
+          hipLaunchKernelGGL((dq_ds_kernel<BF16, DT, CAUSAL, false>), grid, dim3(kDqDsWaves * 64), 0, st, a);
+      }
+      return hipGetLastError();
+    }
+  }
   // order: standalone delta (bit 0), dQ (bit 2; also writes delta), then dK/dV (bit 1, reads it)
   if (stages & 1) {
     dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
@@ -721,7 +977,7 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   }
   if (stages & 2) {
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 1
+#define FA2_ABI_VERSION 2
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -104,6 +104,12 @@ typedef struct fa2_bwd_args {
   float softmax_scale;
   float dropout_p;
   uint64_t dropout_seed;
+  /* optional dS workspace (ABI 2): when non-NULL and at least fa2_bwd_ds_workspace_bytes(args)
+   * bytes, dK/dV also stores the rounded dS = P (dP - delta) tiles it computes, and dQ = dS K
+   * becomes a streaming pass over them instead of a second recompute of S and dP.  NULL keeps
+   * the recompute dQ kernel.  Contents are scratch (no initialisation needed). */
+  void* ds_workspace;
+  int64_t ds_workspace_bytes;
 } fa2_bwd_args;
 
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
@@ -113,8 +119,12 @@ int fa2_bwd(const fa2_bwd_args* args, void* stream);
  * Launch order: bit 0 delta = rowsum(O * dO) (standalone kernel), bit 2 dQ (which also computes
  * delta for its rows and writes it to args->delta), bit 1 dK/dV (reads delta).  A mask must
  * produce delta before dK/dV reads it (bit 0 or bit 2, now or in an earlier call);
- * fa2_bwd == fa2_bwd_stages(args, 6, stream). */
+ * fa2_bwd == fa2_bwd_stages(args, 6, stream) without a dS workspace, 7 with one. */
 int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
+/* Bytes of dS workspace the backward can use for these arguments (0: the dS path does not
+ * apply: head_dim not a multiple of 8, <= 32 or > 128).  With a workspace the launch order is
+ * bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and fa2_bwd runs all three. */
+int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* args);
 
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,
  * row stride mask_row_stride bytes).  Replaces attention_mask.sum(1).cumsum(0) and the

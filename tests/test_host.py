@@ -17,12 +17,12 @@ HEADER = open(os.path.join(ROOT, "include", "fa2_amd.h")).read()
 
 
 def test_library_exports_every_header_symbol():
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(fa2_\w+)\s*\(", HEADER, flags=re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(fa2_\w+)\s*\(", HEADER, flags=re.M))
     assert declared == set(_lib.EXPORTED_SYMBOLS)
     lib = _lib.load()
     for sym in declared:
         assert hasattr(lib, sym), sym
-    assert lib.fa2_version() == 1
+    assert lib.fa2_version() == _lib.ABI_VERSION == int(re.search(r"FA2_ABI_VERSION (\d+)", HEADER).group(1))
 
 
 def _header_struct_fields(name):
@@ -64,6 +64,36 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fa2_bwd(ctypes.byref(b), None) == _lib.FA2_E_UNSUPPORTED
     with pytest.raises(NotImplementedError):
         _lib.check(_lib.FA2_E_UNSUPPORTED)
+
+
+@pytest.mark.parametrize("b,hq,sq,sk,d", [(8, 32, 4096, 4096, 128), (2, 32, 8192, 8192, 128), (3, 4, 517, 203, 64),
+                                           (1, 2, 33, 1, 256), (2, 2, 100, 100, 32), (2, 2, 100, 100, 72),
+                                           (2, 2, 100, 100, 111)])
+def test_ds_workspace_bytes_matches_library(b, hq, sq, sk, d):
+    from fa2_triton_amd.backward import ds_workspace_bytes
+
+    lib = _lib.load()
+    a = _lib.BwdArgs()
+    a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = b, hq, 1, sq, sk, d
+    q, k = torch.empty(b, sq, hq, d, device="meta"), torch.empty(b, sk, 1, d, device="meta")
+    assert lib.fa2_bwd_ds_workspace_bytes(ctypes.byref(a)) == ds_workspace_bytes(q, k)
+    if d % 8 == 0 and 32 < d <= 128:
+        assert ds_workspace_bytes(q, k) == b * hq * -(-sq // 32) * -(-sk // 32) * 2048
+    else:
+        assert ds_workspace_bytes(q, k) == 0
+
+
+def test_ds_workspace_is_validated_without_a_gpu():
+    lib = _lib.load()
+    a = _lib.BwdArgs()
+    a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = 1, 2, 2, 64, 64, 128
+    a.dtype, a.dq_dtype, a.lse_row_stride = _lib.FA2_BF16, _lib.FA2_BF16, 128
+    for name in ("q", "k", "v", "o", "dout", "lse", "delta", "dq", "dk", "dv"):
+        setattr(a, name, 4096)  # never dereferenced: validation fails first
+    a.ds_workspace, a.ds_workspace_bytes = 4096, 1024
+    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"ds_workspace_bytes" in lib.fa2_last_error()
+    a.head_dim, a.ds_workspace_bytes = 111, 1 << 30
+    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"does not apply" in lib.fa2_last_error()
 
 
 def test_infer_bias_strides():
