@@ -39,6 +39,16 @@
 #ifndef FA2_DS_ST_NT
 #define FA2_DS_ST_NT 1  // dS workspace stores non-temporal (measured 1.5 % faster dK/dV)
 #endif
+#ifndef FA2_DS_ST_POL
+#define FA2_DS_ST_POL 0  // dS stores by asm with cache policy: 1 sc1, 2 sc0 sc1, 3 sc1 nt (0: builtin)
+#endif
+#if FA2_DS_ST_POL == 1
+#define FA2_DS_ST_POLICY "sc1"
+#elif FA2_DS_ST_POL == 2
+#define FA2_DS_ST_POLICY "sc0 sc1"
+#elif FA2_DS_ST_POL == 3
+#define FA2_DS_ST_POLICY "sc1 nt"
+#endif
 #ifndef FA2_DS_ABL
 #define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs
 #endif
@@ -334,7 +344,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       char* dst = (char*)p.ds_workspace + chunk * kDsChunk + r32 * 64 + 32 * hh;
 #pragma unroll
       for (int sp = 0; sp < 2 && !(FA2_DS_ABL & 1); ++sp) {
-#if FA2_DS_ST_NT
+#ifdef FA2_DS_ST_POLICY
+        asm volatile("global_store_dwordx4 %0, %1, off " FA2_DS_ST_POLICY :: "v"(dst + 16 * sp), "v"(dsp[sp]) : "memory");
+#elif FA2_DS_ST_NT
         __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
 #else
         *(u32x4*)(dst + 16 * sp) = dsp[sp];
