@@ -49,6 +49,9 @@
 #elif FA2_DS_ST_POL == 3
 #define FA2_DS_ST_POLICY "sc1 nt"
 #endif
+#ifndef FA2_DS_ST_LATE
+#define FA2_DS_ST_LATE 0  // dS stores after the step's dV/dK MFMAs instead of before them
+#endif
 #ifndef FA2_DS_ABL
 #define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs
 #endif
@@ -69,7 +72,14 @@ namespace fa2 {
 
 constexpr int kDsChunk = 32 * 32 * 2;  // bytes of one 32-key x 32-query dS tile in the workspace
 constexpr int kDqDsWaves = 8;          // dq_ds_kernel: waves (32 query rows each) per workgroup
-constexpr int kDqDsStages = 3;         // dq_ds_kernel: K + dS tiles in LDS (two in flight)
+#ifndef FA2_DQDS_BN
+#define FA2_DQDS_BN 32
+#endif
+#ifndef FA2_DQDS_STAGES
+#define FA2_DQDS_STAGES 4
+#endif
+constexpr int kDqDsBN = FA2_DQDS_BN;          // dq_ds_kernel: keys per tile (D > 64)
+constexpr int kDqDsStages = FA2_DQDS_STAGES;  // dq_ds_kernel: ring of K + dS tiles in LDS
 
 // ---------------------------------------------------------------------------------------------
 // delta[b, h, i] = sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows)
@@ -290,6 +300,27 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       hi = qhi - m - 4 * hh;
     }
     u32x4 pp[2], dsp[2];
+    auto store_ds = [&]() {
+      // publish the rounded dS tile for dq_ds_kernel: chunk (b, hq, q-tile m/32, key block
+      // kw0/32) = 32 key rows of 64 bytes; row kj holds this lane pair's registers as they are
+      // (bytes 32 hh + 16 sp: dsp[sp] = queries 16 sp + 8 (t >> 2) + 4 hh + (t & 3), t = 0..7),
+      // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
+      // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
+      // made dq_ds_kernel's gather 10 % slower.)
+      const int64_t chunk = ((int64_t)(b * p.heads_q + hq) * ((p.seqlen_q + 31) >> 5) + (m >> 5)) *
+                                ((p.seqlen_k + 31) >> 5) + (kw0 >> 5);
+      char* dst = (char*)p.ds_workspace + chunk * kDsChunk + r32 * 64 + 32 * hh;
+#pragma unroll
+      for (int sp = 0; sp < 2 && !(FA2_DS_ABL & 1); ++sp) {
+#ifdef FA2_DS_ST_POLICY
+        asm volatile("global_store_dwordx4 %0, %1, off " FA2_DS_ST_POLICY :: "v"(dst + 16 * sp), "v"(dsp[sp]) : "memory");
+#elif FA2_DS_ST_NT
+        __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
+#else
+        *(u32x4*)(dst + 16 * sp) = dsp[sp];
+#endif
+      }
+    };
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 l4 = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh));
@@ -332,27 +363,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
-    if constexpr (DSOUT) {
-      // publish the rounded dS tile for dq_ds_kernel: chunk (b, hq, q-tile m/32, key block
-      // kw0/32) = 32 key rows of 64 bytes; row kj holds this lane pair's registers as they are
-      // (bytes 32 hh + 16 sp: dsp[sp] = queries 16 sp + 8 (t >> 2) + 4 hh + (t & 3), t = 0..7),
-      // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
-      // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
-      // made dq_ds_kernel's gather 10 % slower.)
-      const int64_t chunk = ((int64_t)(b * p.heads_q + hq) * ((p.seqlen_q + 31) >> 5) + (m >> 5)) *
-                                ((p.seqlen_k + 31) >> 5) + (kw0 >> 5);
-      char* dst = (char*)p.ds_workspace + chunk * kDsChunk + r32 * 64 + 32 * hh;
-#pragma unroll
-      for (int sp = 0; sp < 2 && !(FA2_DS_ABL & 1); ++sp) {
-#ifdef FA2_DS_ST_POLICY
-        asm volatile("global_store_dwordx4 %0, %1, off " FA2_DS_ST_POLICY :: "v"(dst + 16 * sp), "v"(dsp[sp]) : "memory");
-#elif FA2_DS_ST_NT
-        __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
-#else
-        *(u32x4*)(dst + 16 * sp) = dsp[sp];
-#endif
-      }
-    }
+    if constexpr (DSOUT && !FA2_DS_ST_LATE) store_ds();
     __builtin_amdgcn_sched_barrier(0);
 #if FA2_DKDV_LEAD
     {
@@ -385,6 +396,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
     }
 #endif
+    if constexpr (DSOUT && FA2_DS_ST_LATE) store_ds();
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
@@ -813,12 +825,14 @@ template <bool BF16, int DT, bool CAUSAL, bool DQF32>
 __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NW = kDqDsWaves, NT = NW * 64;
-  constexpr int BM = NW * 32, BN = 64;
+  constexpr int BN = DT > 64 ? kDqDsBN : 64;  // keys per tile (K pieces must cover every lane)
+  constexpr int BM = NW * 32, HB = BN / 32;
   constexpr int NDT = DT / 32;
-  constexpr int NBUF = kDqDsStages;
   constexpr int KTILE = BN * DT * 2;        // K tile bytes
-  constexpr int DSW = 2 * kDsChunk;         // one wave's dS image of a tile: 64 keys x 32 queries
+  constexpr int DSW = HB * kDsChunk;        // one wave's dS image of a tile: BN keys x 32 queries
   constexpr int BUF = KTILE + NW * DSW;
+  constexpr int NBUF = kDqDsStages < (160 * 1024) / BUF ? kDqDsStages : (160 * 1024) / BUF;
+  static_assert(NBUF >= 3 && NBUF <= 6, "ring of 3..6 buffers");
   constexpr int KP = BufStager<DT, BN, NT>::kIters;  // K pieces per lane and tile
   static_assert(BufStager<DT, BN, NT>::kPieces % NT == 0, "every lane issues the same K pieces");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
@@ -866,9 +880,9 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
                               (uint32_t)min(nkt, (nw_end + 31) >> 5) * kDsChunk);
   // piece it (0..3) of this lane: 16 bytes of the 4 KB image of two chunks; the image is a
   // Tile<32, 64> ([64 keys][32 query columns], swizzled 16-byte chunks), the source row-major
-  uint32_t doff[4];
+  uint32_t doff[2 * HB];
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < 2 * HB; ++it) {
     const int pc = it * 64 + lane;
     const int pr = pc >> 2;                          // key row 0..63 of the image
     const int cc = (pc & 3) ^ ((pr >> 2) & 3);       // 16-byte column chunk stored at this position
@@ -879,7 +893,7 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
     const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(dtile(buf)));
     const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(n >> 5) * kDsChunk);
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < 2 * HB; ++it) {
       uint32_t keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen " FA2_DS_LD_POLICY "lds\n\ts_mov_b32 m0, %0"
@@ -888,28 +902,35 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
           : "memory");
     }
   };
-  constexpr int VM = KP + 4;  // VMEM ops per lane and stage: vmcnt(VM) leaves one stage in flight
-  static_assert(NBUF == 3, "the ring below keeps two stages in flight");
-  if (ntiles > 0) stage(0, 0);
-  if (ntiles > 1) stage(1, BN);
+  constexpr int VM = KP + 2 * HB;  // VMEM ops per lane and stage
+  // wait until at most `pending` stages (the youngest) are in flight, then a raw barrier:
+  // __syncthreads() would drain the tiles in flight
+  auto wait_keep = [&](int pending) {
+    if (pending >= 4 && NBUF >= 6) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(4 * VM) : "memory");
+    else if (pending >= 3 && NBUF >= 5) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(3 * VM) : "memory");
+    else if (pending >= 2 && NBUF >= 4) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(2 * VM) : "memory");
+    else if (pending >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < ntiles) stage(j, j * BN);
 
   f32x16 acc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
-  // raw barriers with counted waits: __syncthreads() would drain the tiles in flight
-  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  wait_keep(min(NBUF - 2, ntiles - 1));  // tile 0 landed
 
   int cur = 0;
   for (int it = 0; it < ntiles; ++it) {
     const int n0 = it * BN;
-    // tile it + 2 goes into the buffer tile it - 1 used (every wave is past its last read)
-    const int nxt2 = cur == 0 ? 2 : cur - 1;
-    if (it + 2 < ntiles) stage(nxt2, n0 + 2 * BN);
+    // tile it + NBUF - 1 goes into the buffer tile it - 1 used (every wave is past its last read)
+    const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
+    if (it + NBUF - 1 < ntiles) stage(nxt, n0 + (NBUF - 1) * BN);
     const char* K = ktile(cur);
     const char* T = dtile(cur);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < HB; ++t) {
       if ((FA2_DS_ABL & 2) || n0 + 32 * t >= nw_end) break;  // wave-uniform: chunk not written
       constexpr int N = 2 * NDT;
       u32x4 fb[2], fa[N];
@@ -920,9 +941,8 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
 #pragma unroll
       for (int m = 0; m < N; ++m) acc[m % NDT] = E::mfma(fa[m], fb[m / NDT], acc[m % NDT]);
     }
-    // tile it + 1 must have landed; tile it + 2 may stay in flight
-    if (it + 2 < ntiles) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // tile it + 1 must have landed; the stages issued after it may stay in flight
+    wait_keep(min(NBUF - 2, ntiles - it - 2));
     cur = cur == NBUF - 1 ? 0 : cur + 1;
   }
 
