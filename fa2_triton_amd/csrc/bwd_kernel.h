@@ -53,7 +53,8 @@
 #define FA2_DS_ST_LATE 0  // dS stores after the step's dV/dK MFMAs instead of before them
 #endif
 #ifndef FA2_DS_ABL
-#define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs
+#define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs,
+                      // 4 = half the dS stores, 8 = dS stores to 256 L2-resident tiles
 #endif
 #ifndef FA2_DS_LD_POLICY
 #define FA2_DS_LD_POLICY "nt "  // cache policy of the dS workspace loads (once-read stream)
@@ -309,9 +310,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // made dq_ds_kernel's gather 10 % slower.)
       const int64_t chunk = ((int64_t)(b * p.heads_q + hq) * ((p.seqlen_q + 31) >> 5) + (m >> 5)) *
                                 ((p.seqlen_k + 31) >> 5) + (kw0 >> 5);
-      char* dst = (char*)p.ds_workspace + chunk * kDsChunk + r32 * 64 + 32 * hh;
+      char* dst = (char*)p.ds_workspace + ((FA2_DS_ABL & 8) ? (int64_t)(blockIdx.x & 255) : chunk) * kDsChunk + r32 * 64 + 32 * hh;
 #pragma unroll
-      for (int sp = 0; sp < 2 && !(FA2_DS_ABL & 1); ++sp) {
+      for (int sp = 0; sp < ((FA2_DS_ABL & 4) ? 1 : 2) && !(FA2_DS_ABL & 1); ++sp) {
 #ifdef FA2_DS_ST_POLICY
         asm volatile("global_store_dwordx4 %0, %1, off " FA2_DS_ST_POLICY :: "v"(dst + 16 * sp), "v"(dsp[sp]) : "memory");
 #elif FA2_DS_ST_NT
@@ -434,7 +435,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // the 2 dS stores of this step were issued after the next tile's LDS-DMA: wait for all
       // but them (vmcnt retires in issue order) and use a raw barrier, whose __syncthreads()
       // form would drain the stores too; they complete under the next step
-      if ((FA2_DS_ABL & 1) || __builtin_amdgcn_readfirstlane(dead))
+      if ((FA2_DS_ABL & 5) || __builtin_amdgcn_readfirstlane(dead))
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
