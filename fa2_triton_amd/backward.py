@@ -24,10 +24,10 @@ from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_drop
 def ds_workspace_bytes(q: Tensor, k: Tensor) -> int:
     """Bytes of the dS workspace (`fa2_bwd_ds_workspace_bytes`): one 2 KiB tile of rounded
     dS per (batch, q-head, 32-query tile, 32-key tile); 0 where the path does not apply
-    (head_dim not a multiple of 8, <= 32 or > 128)."""
+    (head_dim not a multiple of 8, <= 64 or > 128: at D <= 64 the recompute dQ kernel is faster)."""
     batch, seqlen_q, nheads_q, head_dim = q.shape
     seqlen_k = k.shape[1]
-    if head_dim % 8 != 0 or head_dim <= 32 or head_dim > 128 or seqlen_q == 0 or seqlen_k == 0:
+    if head_dim % 8 != 0 or head_dim <= 64 or head_dim > 128 or seqlen_q == 0 or seqlen_k == 0:
         return 0
     return batch * nheads_q * math.ceil(seqlen_q / 32) * math.ceil(seqlen_k / 32) * 2048
 

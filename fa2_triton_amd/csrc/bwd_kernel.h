@@ -973,7 +973,7 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
 // ---------------------------------------------------------------------------------------------
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
-  if constexpr (ALIGNED && (DT == 64 || DT == 128)) {
+  if constexpr (ALIGNED && DT == 128) {  // head dims 72..128 (fa2_bwd_ds_workspace_bytes)
     if (a.ds_workspace) {
       // dS path: delta (bit 0), dK/dV + dS tiles (bit 1), dQ = dS K (bit 2)
       if (stages & 1) {

@@ -122,7 +122,7 @@ int fa2_bwd(const fa2_bwd_args* args, void* stream);
  * fa2_bwd == fa2_bwd_stages(args, 6, stream) without a dS workspace, 7 with one. */
 int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
 /* Bytes of dS workspace the backward can use for these arguments (0: the dS path does not
- * apply: head_dim not a multiple of 8, <= 32 or > 128).  With a workspace the launch order is
+ * apply: head_dim not a multiple of 8, <= 64 or > 128).  With a workspace the launch order is
  * bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and fa2_bwd runs all three. */
 int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* args);
 

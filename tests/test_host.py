@@ -77,7 +77,7 @@ def test_ds_workspace_bytes_matches_library(b, hq, sq, sk, d):
     a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = b, hq, 1, sq, sk, d
     q, k = torch.empty(b, sq, hq, d, device="meta"), torch.empty(b, sk, 1, d, device="meta")
     assert lib.fa2_bwd_ds_workspace_bytes(ctypes.byref(a)) == ds_workspace_bytes(q, k)
-    if d % 8 == 0 and 32 < d <= 128:
+    if d % 8 == 0 and 64 < d <= 128:
         assert ds_workspace_bytes(q, k) == b * hq * -(-sq // 32) * -(-sk // 32) * 2048
     else:
         assert ds_workspace_bytes(q, k) == 0
