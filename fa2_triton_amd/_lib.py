@@ -96,10 +96,12 @@ class BwdArgs(ctypes.Structure):
         ("dropout_seed", ctypes.c_uint64),
         ("ds_workspace", ctypes.c_void_p),
         ("ds_workspace_bytes", ctypes.c_int64),
+        ("dbias", ctypes.c_void_p),
+        ("dbias_stride", _i64x3),
     ]
 
 
-ABI_VERSION = 2  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 3  # FA2_ABI_VERSION in include/fa2_amd.h
 
 EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_ds_workspace_bytes", "fa2_cu_seqlens_from_mask",
                     "fa2_last_error", "fa2_version")

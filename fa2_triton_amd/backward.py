@@ -21,34 +21,55 @@ from . import _lib
 from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, stream_of
 
 
-def ds_workspace_bytes(q: Tensor, k: Tensor) -> int:
-    """Bytes of the dS workspace (`fa2_bwd_ds_workspace_bytes`): one 2 KiB tile of rounded
-    dS per (batch, q-head, 32-query tile, 32-key tile); 0 where the path does not apply
-    (head_dim not a multiple of 8, <= 64 or > 128: at D <= 64 the recompute dQ kernel is faster)."""
+def _fill_args(args, q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, causal: bool) -> None:
+    """The fields of fa2_bwd_args that the dS-workspace query reads: pointers, strides, sizes."""
     batch, seqlen_q, nheads_q, head_dim = q.shape
-    seqlen_k = k.shape[1]
-    if head_dim % 8 != 0 or head_dim <= 64 or head_dim > 128 or seqlen_q == 0 or seqlen_k == 0:
-        return 0
-    return batch * nheads_q * math.ceil(seqlen_q / 32) * math.ceil(seqlen_k / 32) * 2048
+    _, seqlen_k, nheads_kv, _ = k.shape
+    args.q, args.k, args.v, args.o, args.dout = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr()
+    args.q_stride[:] = bshd_strides(q)
+    args.k_stride[:] = bshd_strides(k)
+    args.v_stride[:] = bshd_strides(v)
+    args.o_stride[:] = bshd_strides(o)
+    args.do_stride[:] = bshd_strides(dO)
+    args.batch, args.heads_q, args.heads_kv = batch, nheads_q, nheads_kv
+    args.seqlen_q, args.seqlen_k, args.head_dim = seqlen_q, seqlen_k, head_dim
+    args.causal = int(bool(causal))
+
+
+def ds_workspace_bytes(q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, causal: bool) -> int:
+    """Bytes of the dS workspace (`fa2_bwd_ds_workspace_bytes`): one 2 KiB tile of rounded dS per
+    (batch, q-head, 32-query tile, 32-key tile) with a visible pair (causal: about half the
+    grid); 0 where the path does not apply (head_dim not a multiple of 8, <= 64 or > 128, or
+    tensors without the 16-byte vector layout: the recompute dQ kernel is used instead)."""
+    args = _lib.BwdArgs()
+    _fill_args(args, q, k, v, o, dO, causal)
+    return int(_lib.load().fa2_bwd_ds_workspace_bytes(ctypes.byref(args)))
 
 
 def _ds_workspace_cap(device: torch.device) -> int:
-    """Largest dS workspace the backward allocates by itself: FA2_DS_WORKSPACE_MAX_GB (0
-    disables the dS path), default a quarter of the device's memory (72 GB of a 288 GB MI355X;
-    B=8 H=32 S=4096 needs 8.6 GB)."""
+    """Largest dS workspace the backward allocates by itself: FA2_DS_WORKSPACE_MAX_GB if set (0
+    disables the dS path), otherwise half of the memory available right now -- free device
+    memory plus what torch's caching allocator holds unused -- so that the O(S^2) workspace never
+    takes memory the rest of a training step needs (B=8 H=32 S=4096 causal needs 4.33 GB)."""
     env = os.environ.get("FA2_DS_WORKSPACE_MAX_GB")
     if env is not None:
         return int(float(env) * (1 << 30))
-    return torch.cuda.get_device_properties(device).total_memory // 4
+    free, _ = torch.cuda.mem_get_info(device)
+    cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    return (free + max(cached, 0)) // 2
 
 
-def alloc_ds_workspace(q: Tensor, k: Tensor) -> Optional[Tensor]:
-    """The dS workspace for a backward of these shapes, or None when the dS path does not apply
-    or would exceed the cap (the backward then recomputes S and dP in its dQ kernel)."""
-    nbytes = ds_workspace_bytes(q, k)
+def alloc_ds_workspace(q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, causal: bool) -> Optional[Tensor]:
+    """The dS workspace for a backward of these tensors, or None when the dS path does not
+    apply, would exceed the cap, or cannot be allocated: the backward then recomputes S and dP
+    in its dQ kernel (O(S) memory, as the reference's backward)."""
+    nbytes = ds_workspace_bytes(q, k, v, o, dO, causal)
     if nbytes == 0 or nbytes > _ds_workspace_cap(q.device):
         return None
-    return torch.empty(nbytes, dtype=torch.uint8, device=q.device)
+    try:
+        return torch.empty(nbytes, dtype=torch.uint8, device=q.device)
+    except torch.OutOfMemoryError:
+        return None
 
 
 def _flash_attn_backward(
@@ -69,7 +90,12 @@ def _flash_attn_backward(
     _delta: Optional[Tensor] = None,
     _ds_ws: Optional[Tensor] = None,
     _use_ds: Optional[bool] = None,
-) -> Tuple[Tensor, Tensor, Tensor]:
+    bias_grad: bool = False,
+):
+    """Returns (dq, dk, dv) -- the reference's contract -- or (dq, dk, dv, dbias) with
+    `bias_grad=True`: dbias = dL/d(bias) in bias's shape and dtype, the fp32 dS the dK/dV kernel
+    writes per (batch, q-head) summed over the bias's broadcast dims (deterministic).  The
+    reference has no bias gradient (/root/reference/src/wrapper.py:86 returns None)."""
     if attention_mask is not None:
         assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
         assert q.size(1) == k.size(1), "Attention mask is not supported with seqlen_q != seqlen_k"
@@ -94,24 +120,23 @@ def _flash_attn_backward(
     delta = torch.empty_like(lse) if _delta is None else _delta  # workspace: rowsum(O * dO)
 
     args = _lib.BwdArgs()
-    args.q, args.k, args.v, args.o, args.dout = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr()
+    _fill_args(args, q, k, v, o, dO, causal)
     args.lse, args.delta = lse.data_ptr(), delta.data_ptr()
     args.dq, args.dk, args.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
     args.bias = bias.data_ptr() if bias is not None else None
     args.cu_seqlens = cu_seqlens.data_ptr() if cu_seqlens is not None else None
-    args.q_stride[:] = bshd_strides(q)
-    args.k_stride[:] = bshd_strides(k)
-    args.v_stride[:] = bshd_strides(v)
-    args.o_stride[:] = bshd_strides(o)
-    args.do_stride[:] = bshd_strides(dO)
     args.dq_stride[:] = bshd_strides(dq)
     args.dk_stride[:] = bshd_strides(dk)
     args.dv_stride[:] = bshd_strides(dv)
     args.bias_stride[:] = (stride_bb, stride_bh, stride_bm)
-    args.batch, args.heads_q, args.heads_kv = batch, nheads_q, nheads_kv
-    args.seqlen_q, args.seqlen_k, args.head_dim = seqlen_q, seqlen_k, head_dim
     args.lse_row_stride = lse_rows
-    args.causal = int(bool(causal))
+    dbias_full = None
+    if bias_grad:
+        assert bias is not None, "bias_grad needs a bias"
+        # [B, Hq, Sq, Sk] fp32, zero where no (query, key) pair is visible
+        dbias_full = torch.zeros(batch, nheads_q, seqlen_q, seqlen_k, dtype=torch.float32, device=q.device)
+        args.dbias = dbias_full.data_ptr()
+        args.dbias_stride[:] = dbias_full.stride()[:3]
     args.dtype = encode_dtype(q)
     args.bias_dtype = encode_dtype(bias) if bias is not None else 0
     args.dq_dtype = encode_dtype(dq)
@@ -123,11 +148,15 @@ def _flash_attn_backward(
     if _use_ds is False:
         ds_ws = None
     else:
-        ds_ws = _ds_ws if _ds_ws is not None else alloc_ds_workspace(q, k)
+        ds_ws = _ds_ws if _ds_ws is not None else alloc_ds_workspace(q, k, v, o, dO, causal)
     if ds_ws is not None:
         args.ds_workspace, args.ds_workspace_bytes = ds_ws.data_ptr(), ds_ws.numel() * ds_ws.element_size()
     stages = _stages if _stages is not None else (7 if ds_ws is not None else 6)
     lib = _lib.load()
     with torch.cuda.device(q.device):
         _lib.check(lib.fa2_bwd_stages(ctypes.byref(args), stages, stream_of(q)))
-    return dq, dk, dv
+    if not bias_grad:
+        return dq, dk, dv
+    dims = [i for i in (0, 1) if bias.size(i) == 1]
+    dbias = dbias_full.sum(dim=dims, keepdim=True) if dims else dbias_full
+    return dq, dk, dv, dbias.to(bias.dtype)

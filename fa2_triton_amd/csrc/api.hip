@@ -76,7 +76,9 @@ int fa2_fwd(const fa2_fwd_args* a, void* stream) {
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
   if (rc) return rc;
-  if (!a->q || !a->k || !a->v || !a->o || !a->lse) return fail(FA2_E_INVALID, "null tensor pointer");
+  // an empty side may come with null pointers (torch gives size-0 tensors data_ptr 0)
+  const bool qs = a->seqlen_q > 0, ks = a->seqlen_k > 0;
+  if ((qs && (!a->q || !a->o || !a->lse)) || (ks && (!a->k || !a->v))) return fail(FA2_E_INVALID, "null tensor pointer");
   if (a->bias && a->bias_dtype != FA2_F16 && a->bias_dtype != FA2_BF16 && a->bias_dtype != FA2_F32)
     return fail(FA2_E_INVALID, "bias dtype %d", a->bias_dtype);
   if (a->seqlen_q == 0) return FA2_OK;
@@ -105,13 +107,15 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
   if (rc) return rc;
-  if (!a->q || !a->k || !a->v || !a->o || !a->dout || !a->lse || !a->delta || !a->dq || !a->dk || !a->dv)
+  const bool qs = a->seqlen_q > 0, ks = a->seqlen_k > 0;
+  if ((qs && (!a->q || !a->o || !a->dout || !a->lse || !a->delta || !a->dq)) || (ks && (!a->k || !a->v || !a->dk || !a->dv)))
     return fail(FA2_E_INVALID, "null tensor pointer");
   if (a->dq_dtype != a->dtype && a->dq_dtype != FA2_F32) return fail(FA2_E_INVALID, "dq dtype %d", a->dq_dtype);
   if (a->bias && a->bias_dtype != FA2_F16 && a->bias_dtype != FA2_BF16 && a->bias_dtype != FA2_F32)
     return fail(FA2_E_INVALID, "bias dtype %d", a->bias_dtype);
   if (stages & ~7) return fail(FA2_E_INVALID, "stage mask %d", stages);
-  if (a->seqlen_q == 0 && a->seqlen_k == 0) return FA2_OK;
+  if (a->dbias && !a->bias) return fail(FA2_E_INVALID, "dbias requested without a bias");
+  if (a->seqlen_q == 0 && a->seqlen_k == 0) return FA2_OK;  // empty dQ, dK, dV
   const int D = a->head_dim;
   bool aligned = vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
                  vec_ok(D, a->o, a->o_stride) && vec_ok(D, a->dout, a->do_stride) &&
@@ -123,7 +127,8 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
     aligned = aligned && vec_ok(D, a->dq, a->dq_stride);
   if (a->ds_workspace) {
     const int64_t need = fa2_bwd_ds_workspace_bytes(a);
-    if (need == 0) return fail(FA2_E_INVALID, "ds_workspace given but the dS path does not apply (head_dim %d)", D);
+    if (need == 0)
+      return fail(FA2_E_INVALID, "ds_workspace given but the dS path does not apply (head_dim %d, or unaligned tensors)", D);
     if (a->ds_workspace_bytes < need)
       return fail(FA2_E_INVALID, "ds_workspace_bytes %lld < %lld required", (long long)a->ds_workspace_bytes, (long long)need);
     if (!aligned16(a->ds_workspace)) return fail(FA2_E_INVALID, "ds_workspace must be 16-byte aligned");
@@ -150,10 +155,17 @@ int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, a &&
 int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* a) {
   // head dims 72..128 (multiples of 8): at D <= 64 recomputing S and dP costs less than the dS
   // stream (measured at B=8 H=16 S=1024 D=64: fwd+bwd 0.30 ms recompute, 0.34 ms dS); the
-  // dq_ds_kernel ring of D = 256 tiles would not fit in LDS
+  // dq_ds_kernel ring of D = 256 tiles would not fit in LDS.  The path also needs the 16-byte
+  // vector layout of every tensor it reads (the aligned kernels), so the pointers and strides
+  // of Q, K, V, O and dO must be filled in before this call.
   if (!a || a->head_dim % 8 != 0 || a->head_dim <= 64 || a->head_dim > 128 || a->batch < 1 || a->heads_q < 1) return 0;
   if (a->seqlen_q <= 0 || a->seqlen_k <= 0) return 0;
-  return (int64_t)a->batch * a->heads_q * ((a->seqlen_q + 31) / 32) * ((a->seqlen_k + 31) / 32) * (32 * 32 * 2);
+  const int D = a->head_dim;
+  if (!(vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
+        vec_ok(D, a->o, a->o_stride) && vec_ok(D, a->dout, a->do_stride) && a->k_stride[1] == a->v_stride[1]))
+    return 0;
+  const fa2::DsLayout L(a->seqlen_q, a->seqlen_k, a->causal != 0);
+  return (int64_t)a->batch * a->heads_q * L.per_head() * (32 * 32 * 2);
 }
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,

@@ -318,8 +318,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
       // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
       // made dq_ds_kernel's gather 10 % slower.)
-      const int64_t chunk = ((int64_t)(b * p.heads_q + hq) * ((p.seqlen_q + 31) >> 5) + (m >> 5)) *
-                                ((p.seqlen_k + 31) >> 5) + (kw0 >> 5);
+      const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
+      const int64_t chunk = (int64_t)(b * p.heads_q + hq) * L.per_head() + L.prefix(m >> 5) + (kw0 >> 5);
       char* dst = (char*)p.ds_workspace + ((FA2_DS_ABL & 8) ? (int64_t)(blockIdx.x & 255) : chunk) * kDsChunk + r32 * 64 + 32 * hh;
 #pragma unroll
       for (int sp = 0; sp < ((FA2_DS_ABL & 4) ? 1 : 2) && !(FA2_DS_ABL & 1); ++sp) {
@@ -366,6 +366,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         } else {
           pv[j] = pr;
           dsv[j] = pr * (dp[i] - d4[j]);  // softmax_scale is applied to dK once, at the end
+        }
+        if constexpr (BIAS) {
+          // bias gradient dL/ds_ij = dS (fp32, before rounding): one element per register
+          if (p.dbias != nullptr) {
+            const int qr = m + o + 4 * hh;
+            if (qr < p.seqlen_q && kj < p.seqlen_k)
+              p.dbias[b * p.dbias_stride[0] + hq * p.dbias_stride[1] + (int64_t)qr * p.dbias_stride[2] + kj] = dsv[j];
+          }
         }
 #endif
       }
@@ -892,14 +900,16 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
   BufStager<DT, BN, NT> kst;
   kst.init(tid, p.k_stride[1], D);
   const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
-  // chunk row of query tile j: chunks (b, hq, q-tile, 0 .. nkt) are contiguous; the range ends
+  // chunk row of query tile j: its visible chunks (b, hq, q-tile, 0 .. nvis) are contiguous
+  // (DsLayout, fa2_internal.h); the range ends
   // at the tile's last written chunk, so the DMA of a chunk past it reads zeros and every lane
   // issues the same number of pieces per stage (counted vmcnt below)
-  const int nkt = (p.seqlen_k + 31) >> 5;
+  const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
+  const int nkt = L.nkt;
   i32x4 drs[QT];
 #pragma unroll
   for (int j = 0; j < QT; ++j) {
-    const int64_t crow = ((int64_t)bh * ((p.seqlen_q + 31) >> 5) + ((mw0 >> 5) + j)) * nkt;
+    const int64_t crow = (int64_t)bh * L.per_head() + L.prefix((mw0 >> 5) + j);
     drs[j] = make_rsrc((const char*)p.ds_workspace + crow * kDsChunk,
                        (uint32_t)min(nkt, (nw_end[j] + 31) >> 5) * kDsChunk);
   }
@@ -1015,15 +1025,15 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   if constexpr (ALIGNED && DT == 128) {  // head dims 72..128 (fa2_bwd_ds_workspace_bytes)
     if (a.ds_workspace) {
       // dS path: delta (bit 0), dK/dV + dS tiles (bit 1), dQ = dS K (bit 2)
-      if (stages & 1) {
+      if ((stages & 1) && a.lse_row_stride > 0) {
         dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
         hipLaunchKernelGGL((delta_kernel<BF16, true>), grid, dim3(256), 0, st, a);
       }
-      if (stages & 2) {
+      if ((stages & 2) && a.seqlen_k > 0) {
         dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
         hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a);
       }
-      if (stages & 4) {
+      if ((stages & 4) && a.seqlen_q > 0) {
         constexpr int BM = kDqDsWaves * 32 * DqDsQT<CAUSAL>::value;
         dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
         if (a.dq_dtype == FA2_F32)
@@ -1035,11 +1045,14 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     }
   }
   // order: standalone delta (bit 0), dQ (bit 2; also writes delta), then dK/dV (bit 1, reads it)
-  if (stages & 1) {
+  // zero-sized problems launch nothing for that side: Sk == 0 -> dQ = 0 (dq_kernel sees no key
+  // tile and writes zeros), no dK/dV rows; Sq == 0 -> dK/dV = 0 (dkdv_kernel sees no query
+  // tile and writes zeros), no dQ rows
+  if ((stages & 1) && a.lse_row_stride > 0) {
     dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
   }
-  if (stages & 4) {
+  if ((stages & 4) && a.seqlen_q > 0) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
     dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
@@ -1047,7 +1060,7 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     else
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
-  if (stages & 2) {
+  if ((stages & 2) && a.seqlen_k > 0) {
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
     hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a);
   }

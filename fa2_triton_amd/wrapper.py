@@ -3,7 +3,9 @@
 `flash_attn_func(q, k, v, attention_mask=None, attention_bias=None, dropout_p=0.0,
 causal=False, softmax_scale=None, dropout_seed=None)` with q [B, Sq, Hq, D], k/v
 [B, Sk, Hkv, D] (fp16 / bf16), returns O [B, Sq, Hq, D].  Backward returns (dq, dk, dv) and
-no gradient for the mask, bias and scalars, exactly as the reference (:62-86).
+no gradient for the mask and scalars, exactly as the reference (:62-86).  Beyond the
+reference (which returns None for the bias, :86): when `attention_bias` requires grad, its
+gradient dL/d(bias) is returned too.
 """
 from typing import Optional
 
@@ -52,7 +54,8 @@ class FlashAttnFunc(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, bias, attention_mask, o, lse = ctx.saved_tensors
-        dq, dk, dv = _flash_attn_backward(
+        bias_grad = bias is not None and ctx.needs_input_grad[4]
+        grads = _flash_attn_backward(
             dO=do,
             q=q,
             k=k,
@@ -65,8 +68,10 @@ class FlashAttnFunc(torch.autograd.Function):
             causal=ctx.causal,
             softmax_scale=ctx.softmax_scale,
             dropout_seed=ctx.dropout_seed,
+            bias_grad=bias_grad,
         )
-        return dq, dk, dv, None, None, None, None, None, None
+        dbias = grads[3] if bias_grad else None
+        return grads[0], grads[1], grads[2], None, dbias, None, None, None, None
 
 
 def flash_attn_func(

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 2
+#define FA2_ABI_VERSION 3
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -70,9 +70,10 @@ typedef struct fa2_fwd_args {
   uint64_t dropout_seed;  /* Philox4x32-10 key, identical to Triton's tl.rand */
 } fa2_fwd_args;
 
-/* Backward: dQ, dK, dV of the forward above (dropout_p must be 0, as in the reference,
- * /root/reference/src/utils.py:80-88).  dK/dV are written with heads_kv heads: the GQA
- * group sum is done in fp32 inside the kernel. */
+/* Backward: dQ, dK, dV of the forward above.  dK/dV are written with heads_kv heads: the GQA
+ * group sum is done in fp32 inside the kernel.  dropout_p > 0 is supported (the reference
+ * raises NotImplementedError, /root/reference/src/utils.py:80-88): the kernels regenerate the
+ * forward's Philox keep mask, so dropout_p and dropout_seed must equal the forward's. */
 typedef struct fa2_bwd_args {
   const void* q;
   const void* k;
@@ -104,12 +105,21 @@ typedef struct fa2_bwd_args {
   float softmax_scale;
   float dropout_p;
   uint64_t dropout_seed;
-  /* optional dS workspace (ABI 2): when non-NULL and at least fa2_bwd_ds_workspace_bytes(args)
-   * bytes, dK/dV also stores the rounded dS = P (dP - delta) tiles it computes, and dQ = dS K
-   * becomes a streaming pass over them instead of a second recompute of S and dP.  NULL keeps
-   * the recompute dQ kernel.  Contents are scratch (no initialisation needed). */
+  /* optional dS workspace (ABI 2; causal-compact layout since ABI 3): when non-NULL and at
+   * least fa2_bwd_ds_workspace_bytes(args) bytes, dK/dV also stores the rounded
+   * dS = P (dP - delta) tiles it computes, and dQ = dS K becomes a streaming pass over them
+   * instead of a second recompute of S and dP.  NULL keeps the recompute dQ kernel (O(S)
+   * memory, as the reference).  Contents are scratch (no initialisation needed). */
   void* ds_workspace;
   int64_t ds_workspace_bytes;
+  /* optional bias gradient (ABI 3): when non-NULL (bias must be non-NULL too), dK/dV also
+   * writes dS[b, hq, i, j] = dL/ds_ij = P (dP - delta) in fp32 for every visible (query, key)
+   * pair of every (batch, q-head) into this [B, Hq, Sq, Sk] buffer (element strides below, unit
+   * key stride).  Pairs no kernel visits (fully masked tiles) are not written: zero-fill it
+   * first.  The gradient of a broadcast bias [1|B, 1|Hq, Sq, Sk] is its sum over the broadcast
+   * dims (the reference returns no bias gradient, /root/reference/src/wrapper.py:86). */
+  float* dbias;
+  int64_t dbias_stride[3];
 } fa2_bwd_args;
 
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
@@ -121,9 +131,13 @@ int fa2_bwd(const fa2_bwd_args* args, void* stream);
  * produce delta before dK/dV reads it (bit 0 or bit 2, now or in an earlier call);
  * fa2_bwd == fa2_bwd_stages(args, 6, stream) without a dS workspace, 7 with one. */
 int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
-/* Bytes of dS workspace the backward can use for these arguments (0: the dS path does not
- * apply: head_dim not a multiple of 8, <= 64 or > 128).  With a workspace the launch order is
- * bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and fa2_bwd runs all three. */
+/* Bytes of dS workspace the backward can use for these arguments: 2 KiB per 32 x 32 (query, key)
+ * tile with a visible pair, per (batch, q-head) -- about half the full grid when causal
+ * (B=8 H=32 S=4096 causal: 4.33 GB).  0 when the dS path does not apply: head_dim not a
+ * multiple of 8, <= 64 or > 128, an empty side, or Q/K/V/O/dO not 16-byte aligned with
+ * strides that are multiples of 8 (fill those pointers and strides before calling).  With a
+ * workspace the launch order is bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and
+ * fa2_bwd runs all three. */
 int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* args);
 
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,

@@ -1,0 +1,152 @@
+"""GPU parity for the surfaces the reference grids do not reach.
+
+Each case runs the HIP operator through `flash_attn_func` and checks O, dQ, dK, dV against the
+oracle (oracle/reference.py) with the reference tests' acceptance rule (oracle/tolerance.py):
+* per-head bias [B, Hq, Sq, Sk], [1, Hq, Sq, Sk], [B, 1, Sq, Sk] with GQA, indexed by the query
+  head in forward and backward (the reference uses the kv head in forward,
+  /root/reference/src/forward/kernel.py:141, and rejects per-head bias, src/utils.py:70);
+* an fp32 bias (bias_dtype 32, /root/reference/src/utils.py:102-109);
+* BHSD tensors passed as `x.transpose(1, 2)` views (no copies: unit head_dim stride only,
+  /root/reference/src/wrapper.py:41-43);
+* a data pointer 2 bytes past a 16-byte boundary (the scalar-load path of an aligned head dim);
+* K and V with different sequence strides (the unpipelined forward, the unaligned backward);
+* empty sides: Sk = 0 (O = 0, LSE = -inf, dQ = 0) and Sq = 0 (empty O, dK = dV = 0).
+"""
+import pytest
+import torch
+
+from fa2_triton_amd import flash_attn_func
+from fa2_triton_amd.forward import _flash_attn_forward
+from oracle.reference import attention_reference, lse2_reference
+from oracle.tolerance import check_fa_tolerance
+from tests.core import generate_test_data
+
+
+def _check(q, k, v, do, causal, bias=None, grads_of=None):
+    out = flash_attn_func(q, k, v, None, bias, 0.0, causal)
+    ref = attention_reference(q, k, v, attn_bias=bias, causal=causal)
+    pt = attention_reference(q, k, v, attn_bias=bias, causal=causal, upcast=False, reorder_ops=True)
+    grads = None
+    if grads_of is not None:
+        grads = torch.autograd.grad(out, grads_of, do, retain_graph=True)
+    return check_fa_tolerance(q, k, v, do, out, ref, pt, grads=grads)
+
+
+BIAS_SHAPES = ["b_hq", "1_hq", "b_1", "1_1"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", BIAS_SHAPES)
+@pytest.mark.parametrize("bias_dtype", ["same", "fp32"])
+@pytest.mark.parametrize("d", [64, 128])
+def test_bias_shapes_gqa(dtype, causal, shape, bias_dtype, d):
+    b, hq, hkv, sq, sk = 2, 4, 2, 200, 331
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, d, dtype)
+    bb, bh = {"b_hq": (b, hq), "1_hq": (1, hq), "b_1": (b, 1), "1_1": (1, 1)}[shape]
+    bdt = dtype if bias_dtype == "same" else torch.float32
+    bias = torch.rand(bb, bh, sq, sk, device=q.device, dtype=bdt) * 2 - 1
+    _check(q, k, v, do, causal, bias)
+    # every head really sees its own bias: LSE2 against the oracle's
+    with torch.no_grad():
+        _, lse, _, _ = _flash_attn_forward(q, k, v, None, bias, 0.0, causal, None, None)
+    ref_lse = lse2_reference(q, k, attn_bias=bias, causal=causal)
+    fin = torch.isfinite(ref_lse)
+    torch.testing.assert_close(lse[:, :, :sq][fin], ref_lse[fin], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 96, 128])
+def test_bhsd_transposed_views(causal, d):
+    b, hq, hkv, sq, sk = 2, 4, 2, 257, 190
+    torch.manual_seed(0)
+    dev, dt = "cuda", torch.bfloat16
+    qb = torch.empty(b, hq, sq, d, device=dev, dtype=dt).normal_(0, 0.5)
+    kb = torch.empty(b, hkv, sk, d, device=dev, dtype=dt).normal_(0, 0.5)
+    vb = torch.empty(b, hkv, sk, d, device=dev, dtype=dt).normal_(0, 0.5)
+    q, k, v = (t.transpose(1, 2).requires_grad_() for t in (qb, kb, vb))  # BSHD views of BHSD memory
+    assert not q.is_contiguous() and q.stride(-1) == 1
+    do = torch.randn(b, hq, sq, d, device=dev, dtype=dt).transpose(1, 2)
+    _check(q, k, v, do, causal, grads_of=(q, k, v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("d", [64, 128])
+def test_misaligned_data_pointer(causal, d):
+    b, hq, hkv, sq, sk = 2, 4, 4, 150, 150
+    q0, k0, v0, do = generate_test_data(b, hq, hkv, sq, sk, d, torch.float16)
+
+    def shifted(t):  # same values, data pointer 2 bytes past a 16-byte boundary
+        buf = torch.empty(t.numel() + 1, device=t.device, dtype=t.dtype)
+        x = buf[1:].view(t.shape)
+        x.copy_(t.detach())
+        assert x.data_ptr() % 16 == 2
+        return x.requires_grad_()
+
+    q, k, v = shifted(q0), shifted(k0), shifted(v0)
+    _check(q, k, v, do, causal, grads_of=(q, k, v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_kv_unequal_seq_strides(causal):
+    b, hq, hkv, sq, sk, d = 2, 4, 2, 300, 260, 128
+    q, k0, v, do = generate_test_data(b, hq, hkv, sq, sk, d, torch.bfloat16)
+    wide = torch.zeros(b, sk, 2 * hkv, d, device=q.device, dtype=q.dtype)
+    wide[:, :, :hkv] = k0.detach()
+    k = wide[:, :, :hkv].requires_grad_()  # seq stride 2 Hkv D, V's is Hkv D
+    assert k.stride(1) != v.stride(1)
+    _check(q, k, v, do, causal, grads_of=(q, k, v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_empty_key_side(causal):
+    q, k, v, do = generate_test_data(2, 4, 2, 70, 0, 128, torch.bfloat16)
+    out = flash_attn_func(q, k, v, None, None, 0.0, causal)
+    assert out.shape == q.shape and (out == 0).all()
+    with torch.no_grad():
+        _, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+    assert torch.isneginf(lse[:, :, :70]).all()
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), do)
+    assert (dq == 0).all() and dk.shape == k.shape and dv.shape == v.shape
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_empty_query_side(causal):
+    q, k, v, do = generate_test_data(2, 4, 2, 0, 90, 64, torch.float16)
+    out = flash_attn_func(q, k, v, None, None, 0.0, causal)
+    assert out.shape == q.shape
+    dq, dk, dv = torch.autograd.grad(out, (q, k, v), do)
+    assert dq.shape == q.shape and (dk == 0).all() and (dv == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", BIAS_SHAPES)
+@pytest.mark.parametrize("bias_dtype", ["same", "fp32"])
+def test_bias_gradient(dtype, causal, shape, bias_dtype):
+    """dL/d(bias) (beyond the reference, which returns None) against autograd through the oracle,
+    with the acceptance rule of the other gradients: err <= 3 err_pt + 1e-5, where err_pt is the
+    low-precision PyTorch oracle's error; broadcast dims are summed."""
+    b, hq, hkv, sq, sk, d = 2, 4, 2, 190, 270, 128
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, d, dtype)
+    bb, bh = {"b_hq": (b, hq), "1_hq": (1, hq), "b_1": (b, 1), "1_1": (1, 1)}[shape]
+    bdt = dtype if bias_dtype == "same" else torch.float32
+    bias = (torch.rand(bb, bh, sq, sk, device=q.device, dtype=bdt) * 2 - 1).requires_grad_()
+    out = flash_attn_func(q, k, v, None, bias, 0.0, causal)
+    dq, dk, dv, dbias = torch.autograd.grad(out, (q, k, v, bias), do)
+    assert dbias.shape == bias.shape and dbias.dtype == bias.dtype
+    ref = attention_reference(q, k, v, attn_bias=bias, causal=causal)
+    pt = attention_reference(q, k, v, attn_bias=bias, causal=causal, upcast=False, reorder_ops=True)
+    g_ref = torch.autograd.grad(ref, bias, do, retain_graph=True)[0]
+    g_pt = torch.autograd.grad(pt, bias, do, retain_graph=True)[0]
+    err = (dbias.float() - g_ref.float()).abs().max().item()
+    err_pt = (g_pt.float() - g_ref.float()).abs().max().item()
+    assert err <= 3 * err_pt + 1e-5, (err, err_pt)
+    check_fa_tolerance(q, k, v, do, out, ref, pt, grads=(dq, dk, dv))

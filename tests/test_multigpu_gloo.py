@@ -1,5 +1,6 @@
 """Multi-rank logic of bench.py on CPU (gloo, world_size 2): batch sharding with no data-path
-collective, max-over-ranks timing, whole-job throughput (weak scaling).  The GPU path uses the
+collective, max-over-ranks timing, whole-job throughput (weak and strong scaling), and the
+self-launch of `bench.py --gpus N` (N rank processes, rank 0 prints the line).  The GPU path uses the
 same functions with the nccl (RCCL) backend; only the barrier and the timer reduction are
 collectives."""
 import os
@@ -43,9 +44,46 @@ def test_two_rank_sharding_and_timing():
     assert res[0][2] == res[1][2] == 2.0  # max over ranks
 
 
-def test_job_throughput_is_weak_scaling_aggregate():
+def test_job_throughput_is_whole_job_aggregate():
     f = bench.attn_flops(8, 32, 4096, 4096, 128, True)
-    one, ms1 = bench.job_throughput(f, 10, 1, 0.05)
-    eight, ms8 = bench.job_throughput(f, 10, 8, 0.05)
+    one, ms1 = bench.job_throughput(f, 10, 0.05)
+    eight, ms8 = bench.job_throughput(8 * f, 10, 0.05)  # 8 shards of B=8 in the same time
     assert eight == pytest.approx(8 * one) and ms1 == ms8 == pytest.approx(5.0)
     assert f == pytest.approx(1.0995e12, rel=1e-4)  # BASELINE.md cfg3 fwd FLOP
+
+
+def test_shard_batch_covers_uneven_batches():
+    for gb, world in ((64, 8), (64, 3), (7, 4), (8, 8)):
+        shards = [bench.shard_batch(gb, world, r) for r in range(world)]
+        assert shards[0][0] == 0 and shards[-1][1] == gb
+        assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
+        assert max(h - l for l, h in shards) - min(h - l for l, h in shards) <= 1
+
+
+def _bench_dry_run(*extra):
+    """`python bench.py --gpus 2 --dry-run ...` exactly as a user runs it: the script launches
+    its own 2 rank processes (gloo here, RCCL on the GPU box) and rank 0 prints one line."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    res = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--dry-run", *extra], capture_output=True,
+                         text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # one line, from rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_2_launches_two_ranks_weak():
+    line = _bench_dry_run()
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["global_batch"] == 16
+    assert [tuple(s) for s in line["shards"]] == [(0, 8), (8, 16)]
+    assert line["elapsed"] == pytest.approx(0.002)  # max over the two ranks' timers
+
+
+def test_bench_gpus_2_strong_splits_global_batch():
+    line = _bench_dry_run("--strong", "--global-batch", "64")
+    assert line["scaling"] == "strong" and line["global_batch"] == 64
+    assert [tuple(s) for s in line["shards"]] == [(0, 32), (32, 64)]
