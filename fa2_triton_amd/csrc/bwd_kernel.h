@@ -59,6 +59,9 @@
 #ifndef FA2_DS_LD_POLICY
 #define FA2_DS_LD_POLICY "nt "  // cache policy of the dS workspace loads (once-read stream)
 #endif
+#ifndef FA2_DKDV_PIPE
+#define FA2_DKDV_PIPE 0  // (experiment, slower) head-dim tile 128, aligned, no bias/dropout: dkdv_pipe_kernel.h
+#endif
 #ifndef FA2_DQ_LEAD
 #define FA2_DQ_LEAD 2
 #endif
@@ -194,10 +197,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     qrows = BufStager<DT, BMQ, NT>::max_rows(p.q_stride[1]);
     orows = BufStager<DT, BMQ, NT>::max_rows(p.do_stride[1]);
   }
-  auto stage = [&](int step, int buf) {
-    const int g = step / n_mt, mt = step - g * n_mt;
-    const int hq = hkv * G + g;
-    const int m = m_begin + mt * BMQ;
+  int st_g = 0, st_mt = 0;  // (q-head in group, query tile) of the next step to stage
+  auto stage = [&](int buf) {
+    const int hq = hkv * G + st_g;
+    const int m = m_begin + st_mt * BMQ;
+    if (++st_mt == n_mt) {
+      st_mt = 0;
+      ++st_g;
+    }
     const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
     if constexpr (ALIGNED) {
@@ -223,7 +230,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   if (total > 0) {
     const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
     stage_tile<DT, BNK, NT, ALIGNED>(Vs, vg, p.v_stride[1], n0, Lk, D, tid);
-    stage(0, 0);
+    stage(0);
   }
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
@@ -232,6 +239,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   // Phases (sched_barrier-separated so each phase's LDS fragments stay inside it and the
   // register peak stays under 256): S, dP -> P, dS -> dV, dK.
+  // dS tile of the current step in the workspace (DSOUT): chunk (b, hq, q-tile m / 32, key block
+  // kw0 / 32) of the compact layout (DsLayout), advanced by the visible tiles of each q-tile left
+  const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
+  int64_t ds_head = DSOUT ? (int64_t)(b * p.heads_q + hkv * G) * L.per_head() + L.prefix(m_begin >> 5) + (kw0 >> 5) : 0;
+  int64_t ds_chunk = ds_head;
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
@@ -318,9 +330,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
       // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
       // made dq_ds_kernel's gather 10 % slower.)
-      const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
-      const int64_t chunk = (int64_t)(b * p.heads_q + hq) * L.per_head() + L.prefix(m >> 5) + (kw0 >> 5);
-      char* dst = (char*)p.ds_workspace + ((FA2_DS_ABL & 8) ? (int64_t)(blockIdx.x & 255) : chunk) * kDsChunk + r32 * 64 + 32 * hh;
+      char* dst = (char*)p.ds_workspace + ((FA2_DS_ABL & 8) ? (int64_t)(blockIdx.x & 255) : ds_chunk) * kDsChunk + r32 * 64 + 32 * hh;
 #pragma unroll
       for (int sp = 0; sp < ((FA2_DS_ABL & 4) ? 1 : 2) && !(FA2_DS_ABL & 1); ++sp) {
 #ifdef FA2_DS_ST_POLICY
@@ -432,12 +442,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     __syncthreads();
   }
 
+  int g = 0, mt = 0;  // (q-head in group, query tile) of the current step
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
 #if !(FA2_DKDV_ABL & 2)
-    if (step + 1 < total) stage(step + 1, cur ^ 1);
+    if (step + 1 < total) stage(cur ^ 1);
 #endif
-    const int g = step / n_mt, mt = step - g * n_mt;
     const int hq = hkv * G + g;
     const int m = m_begin + mt * BMQ;
     // wave-uniform tile class
@@ -460,6 +470,13 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     } else {
       vm_wait_all();
       __syncthreads();
+    }
+    if (++mt == n_mt) {
+      mt = 0;
+      ++g;
+      if constexpr (DSOUT) ds_chunk = ds_head += L.per_head();
+    } else if constexpr (DSOUT) {
+      ds_chunk += min(max((m >> 5) + L.c, 0), L.nkt);  // nvis of the q-tile left behind
     }
   }
 
@@ -1030,8 +1047,13 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
         hipLaunchKernelGGL((delta_kernel<BF16, true>), grid, dim3(256), 0, st, a);
       }
       if ((stages & 2) && a.seqlen_k > 0) {
-        dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-        hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a);
+        if (FA2_DKDV_PIPE && !BIAS && !DROPOUT) {
+          const hipError_t e = launch_dkdv_pipe<BF16>(a, true, st);
+          if (e != hipSuccess) return e;
+        } else {
+          dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
+          hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a);
+        }
       }
       if ((stages & 4) && a.seqlen_q > 0) {
         constexpr int BM = kDqDsWaves * 32 * DqDsQT<CAUSAL>::value;
@@ -1061,6 +1083,7 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
   if ((stages & 2) && a.seqlen_k > 0) {
+    if (FA2_DKDV_PIPE && DT == 128 && ALIGNED && !BIAS && !DROPOUT) return launch_dkdv_pipe<BF16>(a, false, st);
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
     hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a);
   }

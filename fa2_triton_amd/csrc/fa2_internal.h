@@ -15,6 +15,11 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st);
 template <bool BF16, int DT>
 hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStream_t st);
 
+// One-wave-per-SIMD software-pipelined dK/dV (dkdv_pipe_kernel.h; head-dim tile 128, aligned,
+// no bias, no dropout); dsout: also store the rounded dS tiles (dS-workspace path).
+template <bool BF16>
+hipError_t launch_dkdv_pipe(const fa2_bwd_args& a, bool dsout, hipStream_t st);
+
 hipError_t launch_cu_seqlens(const uint8_t* mask, int64_t stride, int batch, int seqlen,
                              int32_t* out, hipStream_t st);
 

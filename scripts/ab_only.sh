@@ -1,0 +1,7 @@
+#!/bin/bash
+# GPU: interleaved A/B timing only (no parity run: for ablation builds).  usage: ab_only.sh TAG WHAT CAUSAL libs...
+set -o pipefail
+TAG=$1; WHAT=$2; CAUSAL=$3; shift 3
+mkdir -p gpurun_out/$TAG
+WHAT=$WHAT CAUSAL=$CAUSAL timeout -k 10 300 python scripts/ab.py "$@" > gpurun_out/$TAG/ab.log 2>&1; rc=$?
+cat gpurun_out/$TAG/ab.log; exit $rc

@@ -27,7 +27,11 @@ def counters(sub):
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 
-fetch, write, sq = counters("fetch"), counters("write"), counters("sq")
+fetch, write = counters("fetch"), counters("write")
+sq = collections.defaultdict(dict)
+for sub in ("sq", "sq1", "sq2"):
+    for k, d in counters(sub).items():
+        sq[k].update(d)
 out = {}
 for k in sorted(set(fetch) | set(write) | set(sq)):
     e = {}
@@ -40,6 +44,10 @@ for k in sorted(set(fetch) | set(write) | set(sq)):
     if "fetch_bytes_corrected" in e and "write_bytes" in e:
         e["hbm_bytes_per_launch"] = e["fetch_bytes_corrected"] + e["write_bytes"]
     e.update({c: v for c, v in sq.get(k, {}).items()})
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in e and e.get("GRBM_GUI_ACTIVE"):
+        # MFMA-busy share of every SIMD's cycles: busy cycles (summed over the 1024 SIMDs) over
+        # 1024 x the kernel's GPU-active cycles (GRBM_GUI_ACTIVE sums the 8 XCDs)
+        e["mfma_busy_pct"] = 100.0 * e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * e["GRBM_GUI_ACTIVE"] / 8)
     out[k] = e
 json.dump(out, open(f"{dst}/{tag}_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
