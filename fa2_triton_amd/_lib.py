@@ -98,12 +98,15 @@ class BwdArgs(ctypes.Structure):
         ("ds_workspace_bytes", ctypes.c_int64),
         ("dbias", ctypes.c_void_p),
         ("dbias_stride", _i64x3),
+        ("dkv_workspace", ctypes.c_void_p),
+        ("dkv_workspace_bytes", ctypes.c_int64),
     ]
 
 
-ABI_VERSION = 3  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 4  # FA2_ABI_VERSION in include/fa2_amd.h
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_ds_workspace_bytes", "fa2_cu_seqlens_from_mask",
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_ds_workspace_bytes", "fa2_bwd_dkv_workspace_bytes",
+                    "fa2_cu_seqlens_from_mask",
                     "fa2_last_error", "fa2_version")
 
 _lock = threading.Lock()
@@ -132,6 +135,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_bwd_stages.restype = ctypes.c_int
         lib.fa2_bwd_ds_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
         lib.fa2_bwd_ds_workspace_bytes.restype = ctypes.c_int64
+        lib.fa2_bwd_dkv_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
+        lib.fa2_bwd_dkv_workspace_bytes.restype = ctypes.c_int64
         lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
         lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int

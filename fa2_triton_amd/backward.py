@@ -72,6 +72,20 @@ def alloc_ds_workspace(q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, c
         return None
 
 
+def alloc_dkv_workspace(args, device: torch.device) -> Optional[Tensor]:
+    """fp32 partial-sum workspace of the dK/dV q-head split (`fa2_bwd_dkv_workspace_bytes`), or
+    None when no split applies (Hq == Hkv, or B * Hkv * ceil(Sk / 128) already fills the GPU) or
+    it cannot be allocated (the backward then sums each GQA group in one workgroup).  Small by
+    construction: it only exists when the key-block grid is small."""
+    nbytes = int(_lib.load().fa2_bwd_dkv_workspace_bytes(ctypes.byref(args)))
+    if nbytes == 0 or os.environ.get("FA2_DKV_SPLIT", "1") == "0":
+        return None
+    try:
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    except torch.OutOfMemoryError:
+        return None
+
+
 def _flash_attn_backward(
     dO: Tensor,
     q: Tensor,
@@ -151,6 +165,9 @@ def _flash_attn_backward(
         ds_ws = _ds_ws if _ds_ws is not None else alloc_ds_workspace(q, k, v, o, dO, causal)
     if ds_ws is not None:
         args.ds_workspace, args.ds_workspace_bytes = ds_ws.data_ptr(), ds_ws.numel() * ds_ws.element_size()
+    dkv_ws = alloc_dkv_workspace(args, q.device)
+    if dkv_ws is not None:
+        args.dkv_workspace, args.dkv_workspace_bytes = dkv_ws.data_ptr(), dkv_ws.numel()
     stages = _stages if _stages is not None else (7 if ds_ws is not None else 6)
     lib = _lib.load()
     with torch.cuda.device(q.device):

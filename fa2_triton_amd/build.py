@@ -48,20 +48,6 @@ def generated_sources():
                     with open(path, "w") as f:
                         f.write(body)
                 srcs.append(path)
-    # the one-wave-per-SIMD dK/dV kernel: its own unit, built without the MFMA-VGPR flag so that
-    # the dK/dV accumulators can live in AGPRs (512-register budget)
-    for dname, flag in DTYPES.items():
-        path = os.path.join(GEN, f"bwdp_{dname}.hip")
-        body = (
-            '#include "../dkdv_pipe_kernel.h"\n'
-            "namespace fa2 {\n"
-            f"template hipError_t launch_dkdv_pipe<{flag}>(const fa2_bwd_args&, bool, hipStream_t);\n"
-            "}\n"
-        )
-        if not os.path.exists(path) or open(path).read() != body:
-            with open(path, "w") as f:
-                f.write(body)
-        srcs.append(path)
     return srcs
 
 
@@ -83,8 +69,7 @@ def compile_one(src: str, force: bool, dep_t: float) -> str:
         return obj
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
            "-I", CSRC, "-I", INCLUDE, "-Wno-unused-result"]
-    # MFMA accumulators in arch VGPRs (where the softmax VALU reads them); the one-wave-per-SIMD
-    # dK/dV kernel pins its dK/dV accumulators to AGPRs by asm (dkdv_pipe_kernel.h)
+    # MFMA accumulators in arch VGPRs (where the softmax VALU reads them)
     cmd += ["-mllvm", "-amdgpu-mfma-vgpr-form=true",
            # no SLP packing of the softmax adds into v_pk_add_f32: packed f32 VALU beside MFMAs
            # costs more issue cycles than the scalar pair (MI355X_MICROARCH.md, filler prices)

@@ -133,6 +133,13 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
       return fail(FA2_E_INVALID, "ds_workspace_bytes %lld < %lld required", (long long)a->ds_workspace_bytes, (long long)need);
     if (!aligned16(a->ds_workspace)) return fail(FA2_E_INVALID, "ds_workspace must be 16-byte aligned");
   }
+  if (a->dkv_workspace) {
+    const int64_t need = fa2_bwd_dkv_workspace_bytes(a);
+    if (need == 0) return fail(FA2_E_INVALID, "dkv_workspace given but no dK/dV split applies to these sizes");
+    if (a->dkv_workspace_bytes < need)
+      return fail(FA2_E_INVALID, "dkv_workspace_bytes %lld < %lld required", (long long)a->dkv_workspace_bytes, (long long)need);
+    if (!aligned16(a->dkv_workspace)) return fail(FA2_E_INVALID, "dkv_workspace must be 16-byte aligned");
+  }
   hipStream_t st = (hipStream_t)stream;
   const bool bf = a->dtype == FA2_BF16;
   const int dt = pick_dt(D);
@@ -166,6 +173,11 @@ int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* a) {
     return 0;
   const fa2::DsLayout L(a->seqlen_q, a->seqlen_k, a->causal != 0);
   return (int64_t)a->batch * a->heads_q * L.per_head() * (32 * 32 * 2);
+}
+
+int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* a) {
+  if (!a || a->seqlen_q <= 0 || a->seqlen_k <= 0 || a->head_dim < 1) return 0;
+  return fa2::dkv_workspace_bytes(a->batch, a->heads_q, a->heads_kv, a->seqlen_k, a->head_dim);
 }
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,

@@ -19,60 +19,22 @@
 #include "common.h"
 #include "fa2_internal.h"
 
-// k-steps of fragment reads in flight ahead of their MFMAs (0: compiler order); dK/dV runs at
-// the 256-register limit, where a second step in flight spills
-#ifndef FA2_DKDV_LEAD
-#define FA2_DKDV_LEAD 1
-#endif
-#ifndef FA2_DKDV_SEQ
-#define FA2_DKDV_SEQ 1  // S chain then dP chain with deeper fragment prefetch
-#endif
-#ifndef FA2_DKDV_LS
-#define FA2_DKDV_LS 2  // S-chain fragments in flight (MFMAs ahead)
-#endif
-#ifndef FA2_DKDV_LD
-#define FA2_DKDV_LD 1  // dP-chain fragment pairs in flight
-#endif
-#ifndef FA2_DKDV_ABL
-#define FA2_DKDV_ABL 0  // timing ablations of dK/dV: 1 = no P/dS VALU, 2 = no Q/dO prefetch
-#endif
-#ifndef FA2_DS_ST_NT
-#define FA2_DS_ST_NT 1  // dS workspace stores non-temporal (measured 1.5 % faster dK/dV)
-#endif
-#ifndef FA2_DS_ST_POL
-#define FA2_DS_ST_POL 0  // dS stores by asm with cache policy: 1 sc1, 2 sc0 sc1, 3 sc1 nt (0: builtin)
-#endif
-#if FA2_DS_ST_POL == 1
-#define FA2_DS_ST_POLICY "sc1"
-#elif FA2_DS_ST_POL == 2
-#define FA2_DS_ST_POLICY "sc0 sc1"
-#elif FA2_DS_ST_POL == 3
-#define FA2_DS_ST_POLICY "sc1 nt"
-#endif
-#ifndef FA2_DS_ST_LATE
-#define FA2_DS_ST_LATE 0  // dS stores after the step's dV/dK MFMAs instead of before them
-#endif
-#ifndef FA2_DS_ABL
-#define FA2_DS_ABL 0  // timing ablations of the dS path: 1 = dK/dV without the dS stores, 2 = dQ without MFMAs,
-                      // 4 = half the dS stores, 8 = dS stores to 256 L2-resident tiles
-#endif
-#ifndef FA2_DS_LD_POLICY
-#define FA2_DS_LD_POLICY "nt "  // cache policy of the dS workspace loads (once-read stream)
-#endif
-#ifndef FA2_DKDV_PIPE
-#define FA2_DKDV_PIPE 0  // (experiment, slower) head-dim tile 128, aligned, no bias/dropout: dkdv_pipe_kernel.h
-#endif
-#ifndef FA2_DQ_LEAD
-#define FA2_DQ_LEAD 2
-#endif
-#ifndef FA2_DQ_PIPE
-#define FA2_DQ_PIPE 1  // software-pipelined interior tiles in dq_kernel
-#endif
-#ifndef FA2_DQ_PIPE_LEAD
-#define FA2_DQ_PIPE_LEAD 1
-#endif
+// Schedule constants (measured; the variants they replaced are recorded in DESIGN.md §5):
+//  dK/dV: S chain with its Q fragments kDkdvLS MFMAs ahead, then the dP chain with its
+//         (dO, V) fragment pairs kDkdvLD ahead, then the dV/dK steps two transposed fragments
+//         ahead -- at the 256-register limit a deeper prefetch spills;
+//  dQ (recompute): fragments kDqLead k-steps ahead; interior tiles software-pipelined by
+//         32-key halves with one step of fragments in flight.
+// The dS workspace is written with non-temporal stores (1.5 % faster dK/dV than plain stores;
+// sc1 / sc0 sc1 / sc1 nt: +38 %, +38 %, +75 %) and read with nt LDS-DMA (a once-read stream).
+#define FA2_DS_LD_POLICY "nt "
 
 namespace fa2 {
+
+constexpr int kDkdvLS = 2;
+constexpr int kDkdvLD = 1;
+constexpr int kDqLead = 2;
+constexpr int kDqPipeLead = 1;
 
 constexpr int kDsChunk = 32 * 32 * 2;  // bytes of one 32-key x 32-query dS tile in the workspace
 constexpr int kDqDsWaves = 8;          // dq_ds_kernel: waves (32 query rows each) per workgroup
@@ -140,8 +102,12 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 //   dK^T[d][key] += Q^T dS  NDT*2 MFMA
 // dK/dV accumulate the whole GQA group in fp32 and are rounded once.  <= 256 VGPRs, so two
 // workgroups share a CU (DT <= 128).
+// q-head split (nsplit > 1, small grids: GQA / MQA with few (batch, kv-head, key block) items):
+// the group's q-heads are dealt to nsplit workgroups per key block, each writes its fp32 partial
+// dK/dV sums to p.dkv_workspace ([nsplit][B][Hkv][Sk][D], unscaled) and dkv_reduce_kernel adds
+// them in split order (deterministic).
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED, bool DSOUT>
-__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p, int nsplit) {
   using E = Elem<BF16>;
   constexpr int NT = 256;
   constexpr int BNK = 128;          // keys per workgroup
@@ -157,10 +123,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   const int r32 = lane & 31, hh = lane >> 5;
   const int nkb = (p.seqlen_k + BNK - 1) / BNK;
   const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
-  const int bkv = item / nkb;
-  const int n0 = (item - bkv * nkb) * BNK;           // causal: low keys see the most rows
+  const int grp = item / nkb;                        // (batch, kv-head, q-head split)
+  const int n0 = (item - grp * nkb) * BNK;           // causal: low keys see the most rows
+  const int bkv = grp / nsplit, split = grp - bkv * nsplit;
   const int b = bkv / p.heads_kv, hkv = bkv - b * p.heads_kv;
-  const int G = p.heads_q / p.heads_kv;
+  const int G = p.heads_q / p.heads_kv / nsplit;     // q-heads of this workgroup
+  const int h0 = (hkv * nsplit + split) * G;         // its first q-head
   int Lq = p.seqlen_q, Lk = p.seqlen_k;
   if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
   const int D = p.head_dim;
@@ -199,7 +167,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   }
   int st_g = 0, st_mt = 0;  // (q-head in group, query tile) of the next step to stage
   auto stage = [&](int buf) {
-    const int hq = hkv * G + st_g;
+    const int hq = h0 + st_g;
     const int m = m_begin + st_mt * BMQ;
     if (++st_mt == n_mt) {
       st_mt = 0;
@@ -242,17 +210,16 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   // dS tile of the current step in the workspace (DSOUT): chunk (b, hq, q-tile m / 32, key block
   // kw0 / 32) of the compact layout (DsLayout), advanced by the visible tiles of each q-tile left
   const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
-  int64_t ds_head = DSOUT ? (int64_t)(b * p.heads_q + hkv * G) * L.per_head() + L.prefix(m_begin >> 5) + (kw0 >> 5) : 0;
+  int64_t ds_head = DSOUT ? (int64_t)(b * p.heads_q + h0) * L.per_head() + L.prefix(m_begin >> 5) + (kw0 >> 5) : 0;
   int64_t ds_chunk = ds_head;
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
-#if FA2_DKDV_SEQ
     {
-      // fenced steps: the S chain (one fragment per MFMA, read 3 MFMAs ahead), then the dP
-      // chain (two fragments per MFMA, read 2 ahead): deeper prefetch than alternating chains
+      // fenced steps: the S chain (one fragment per MFMA, read kDkdvLS MFMAs ahead), then the dP
+      // chain (two fragments per MFMA, kDkdvLD ahead): deeper prefetch than alternating chains
       // for the same registers in flight
-      constexpr int LS = FA2_DKDV_LS < KS ? FA2_DKDV_LS : KS, LD = FA2_DKDV_LD < KS ? FA2_DKDV_LD : KS;
+      constexpr int LS = kDkdvLS < KS ? kDkdvLS : KS, LD = kDkdvLD < KS ? kDkdvLD : KS;
       u32x4 fq[KS], fo[KS], fv[KS];
 #pragma unroll
       for (int j = 0; j < LS; ++j) fq[j] = lds_row_frag<DT, BMQ>(Q, 0, r32, j, hh);
@@ -278,36 +245,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#elif FA2_DKDV_LEAD
-    {
-      // fenced steps, S and dP chains alternating, fragments read FA2_DKDV_LEAD k-steps ahead
-      constexpr int L = FA2_DKDV_LEAD < KS ? FA2_DKDV_LEAD : KS;
-      u32x4 fq[KS], fo[KS], fv[KS];
-      auto rd = [&](int ks) {
-        fq[ks] = lds_row_frag<DT, BMQ>(Q, 0, r32, ks, hh);
-        fo[ks] = lds_row_frag<DT, BMQ>(O, 0, r32, ks, hh);
-        fv[ks] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks, hh);
-      };
-#pragma unroll
-      for (int j = 0; j < L; ++j) rd(j);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ks + L < KS) rd(ks + L);
-        s = E::mfma(fq[ks], kf[ks], s);
-        dp = E::mfma(fo[ks], fv[ks], dp);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#else
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BMQ>(Q, 0, r32, ks, hh), kf[ks], s);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      dp = E::mfma(lds_row_frag<DT, BMQ>(O, 0, r32, ks, hh), lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks, hh), dp);
-      if (ks & 1) __builtin_amdgcn_sched_barrier(0);  // at most two fragment pairs in flight
-    }
-#endif
     __builtin_amdgcn_sched_barrier(0);
     // rows of register i: m + (i & 3) + 8 (i >> 2) + 4 hh.  The row window [q_lo, q_hi) of this
     // lane's key is recomputed from an opaque lane id: hoisted out of the loop it gets spilled
@@ -330,17 +267,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
       // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
       // made dq_ds_kernel's gather 10 % slower.)
-      char* dst = (char*)p.ds_workspace + ((FA2_DS_ABL & 8) ? (int64_t)(blockIdx.x & 255) : ds_chunk) * kDsChunk + r32 * 64 + 32 * hh;
+      char* dst = (char*)p.ds_workspace + ds_chunk * kDsChunk + r32 * 64 + 32 * hh;
 #pragma unroll
-      for (int sp = 0; sp < ((FA2_DS_ABL & 4) ? 1 : 2) && !(FA2_DS_ABL & 1); ++sp) {
-#ifdef FA2_DS_ST_POLICY
-        asm volatile("global_store_dwordx4 %0, %1, off " FA2_DS_ST_POLICY :: "v"(dst + 16 * sp), "v"(dsp[sp]) : "memory");
-#elif FA2_DS_ST_NT
-        __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
-#else
-        *(u32x4*)(dst + 16 * sp) = dsp[sp];
-#endif
-      }
+      for (int sp = 0; sp < 2; ++sp) __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
     };
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -359,10 +288,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
           x = fmaf(x, scale2, kLog2e * load_bias(p.bias, b * p.bias_stride[0] + hq * p.bias_stride[1] +
                                                            (int64_t)qc * p.bias_stride[2] + kc, p.bias_dtype));
         }
-#if FA2_DKDV_ABL & 1
-        pv[j] = x;
-        dsv[j] = dp[i];
-#else
         float pr = __builtin_amdgcn_exp2f(fmaf(x, sc, -l4[j]));
         if (MASK) pr = (o >= lo && o < hi) ? pr : 0.f;
         if (DROPOUT) {
@@ -385,19 +310,18 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
               p.dbias[b * p.dbias_stride[0] + hq * p.dbias_stride[1] + (int64_t)qr * p.dbias_stride[2] + kj] = dsv[j];
           }
         }
-#endif
       }
       pp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(pv[0], pv[1]);
       pp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(pv[2], pv[3]);
       dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
-    if constexpr (DSOUT && !FA2_DS_ST_LATE) store_ds();
+    if constexpr (DSOUT) store_ds();
     __builtin_amdgcn_sched_barrier(0);
-#if FA2_DKDV_LEAD
     {
-      // steps m: dt = m % NDT (independent chains back to back), r = m / NDT: (sp, dV | dK)
-      constexpr int N = 4 * NDT, L = 2 * FA2_DKDV_LEAD < N ? 2 * FA2_DKDV_LEAD : N;
+      // steps m: dt = m % NDT (independent chains back to back), r = m / NDT: (sp, dV | dK);
+      // transposed fragments two steps ahead
+      constexpr int N = 4 * NDT, L = 2 < N ? 2 : N;
       u32x4 fr[N];
       auto rd = [&](int m) {
         const int dt = m % NDT, r = m / NDT;
@@ -414,18 +338,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#else
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        dv[dt] = E::mfma(lds_tr_frag<DT, BMQ>(O, 16 * sp, 32 * dt, lane), pp[sp], dv[dt]);
-        dk[dt] = E::mfma(lds_tr_frag<DT, BMQ>(Q, 16 * sp, 32 * dt, lane), dsp[sp], dk[dt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // bound the transposed reads in flight
-    }
-#endif
-    if constexpr (DSOUT && FA2_DS_ST_LATE) store_ds();
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
@@ -445,10 +357,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   int g = 0, mt = 0;  // (q-head in group, query tile) of the current step
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
-#if !(FA2_DKDV_ABL & 2)
     if (step + 1 < total) stage(cur ^ 1);
-#endif
-    const int hq = hkv * G + g;
+    const int hq = h0 + g;
     const int m = m_begin + mt * BMQ;
     // wave-uniform tile class
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
@@ -463,7 +373,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       // the 2 dS stores of this step were issued after the next tile's LDS-DMA: wait for all
       // but them (vmcnt retires in issue order) and use a raw barrier, whose __syncthreads()
       // form would drain the stores too; they complete under the next step
-      if ((FA2_DS_ABL & 5) || __builtin_amdgcn_readfirstlane(dead))
+      if (__builtin_amdgcn_readfirstlane(dead))
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -481,6 +391,41 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   }
 
   // ---- store dK, dV (kv heads; fp32 group sum rounded once) ----------------------------
+  if (nsplit > 1) {
+    // partial sums of this split: [split][b][hkv][key][D] fp32, unscaled (dkv_reduce_kernel)
+    if (kj < p.seqlen_k) {
+      const int64_t row = (((int64_t)split * p.batch + b) * p.heads_kv + hkv) * p.seqlen_k + kj;
+      float* pk = p.dkv_workspace + row * D;
+      float* pv = p.dkv_workspace + ((int64_t)nsplit * p.batch * p.heads_kv * p.seqlen_k + row) * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+          float a[4], c[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[j] = kval ? dk[dt][4 * g4 + j] : 0.f;
+            c[j] = kval ? dv[dt][4 * g4 + j] : 0.f;
+          }
+          if (ALIGNED) {  // D % 8 == 0: whole 4-column groups
+            if (d0 < D) {
+              *(f32x4*)(pk + d0) = f32x4{a[0], a[1], a[2], a[3]};
+              *(f32x4*)(pv + d0) = f32x4{c[0], c[1], c[2], c[3]};
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (d0 + j < D) {
+                pk[d0 + j] = a[j];
+                pv[d0 + j] = c[j];
+              }
+          }
+        }
+      }
+    }
+    return;
+  }
   if (kj < p.seqlen_k) {
     uint16_t* dkrow = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kj * p.dk_stride[1];
     uint16_t* dvrow = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kj * p.dv_stride[1];
@@ -511,6 +456,44 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK/dV of a q-head split (dkdv_kernel, nsplit > 1): dK = scale * sum_s dK_s, dV = sum_s dV_s
+// over the fp32 partials in split order (deterministic), rounded once.  One thread per four
+// columns of one (batch, kv-head, key) row; HBM-bound (2 nsplit fp32 reads per output element).
+template <bool BF16>
+__global__ void __launch_bounds__(256) dkv_reduce_kernel(const fa2_bwd_args p, int nsplit) {
+  using E = Elem<BF16>;
+  const int D = p.head_dim;
+  const int cpr = (D + 3) >> 2;
+  const int64_t rows = (int64_t)p.batch * p.heads_kv * p.seqlen_k;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * cpr) return;
+  const int64_t row = idx / cpr;
+  const int d0 = (int)(idx - row * cpr) * 4;
+  const int kj = (int)(row % p.seqlen_k);
+  const int64_t bh = row / p.seqlen_k;
+  const int hkv = (int)(bh % p.heads_kv), b = (int)(bh / p.heads_kv);
+  const int64_t half = (int64_t)nsplit * rows * D;
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, c[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float* pk = p.dkv_workspace + ((int64_t)s * rows + row) * D + d0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (d0 + j < D) {
+        a[j] += pk[j];
+        c[j] += pk[half + j];
+      }
+  }
+  uint16_t* dkrow = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kj * p.dk_stride[1];
+  uint16_t* dvrow = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kj * p.dv_stride[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (d0 + j < D) {
+      dkrow[d0 + j] = E::from_f32(a[j] * p.softmax_scale);
+      dvrow[d0 + j] = E::from_f32(c[j]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -646,9 +629,8 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     for (int t = 0; t < 2; ++t) {
       if (MASK && !(n0 + 32 * t < Lk && (!CAUSAL || n0 + 32 * t <= mw0 + 31 + diag))) continue;
       f32x16 s = zero16(), dp = zero16();
-#if FA2_DQ_LEAD
       {
-        constexpr int L = FA2_DQ_LEAD < KS ? FA2_DQ_LEAD : KS;
+        constexpr int L = kDqLead < KS ? kDqLead : KS;
         u32x4 fk[KS], fv[KS];
         auto rd = [&](int ks) {
           fk[ks] = lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh);
@@ -664,13 +646,6 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
-#endif
       __builtin_amdgcn_sched_barrier(0);
       u32x4 dsp[2];
 #pragma unroll
@@ -702,9 +677,8 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
         for (int j = 0; j < 4; ++j) dsp[sp][j] = E::pack2(dsv[2 * j], dsv[2 * j + 1]);
       }
       __builtin_amdgcn_sched_barrier(0);
-#if FA2_DQ_LEAD
       {
-        constexpr int N = 2 * NDT, L = 2 * FA2_DQ_LEAD < N ? 2 * FA2_DQ_LEAD : N;
+        constexpr int N = 2 * NDT, L = 2 * kDqLead < N ? 2 * kDqLead : N;
         u32x4 fr[N];
         auto rd = [&](int m) { return lds_tr_frag<DT, BN>(K, 32 * t + 16 * (m / NDT), 32 * (m % NDT), lane); };
 #pragma unroll
@@ -716,15 +690,6 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp)
-          acc[dt] = E::mfma(lds_tr_frag<DT, BN>(K, 32 * t + 16 * sp, 32 * dt, lane), dsp[sp], acc[dt]);
-        if (dt & 1) __builtin_amdgcn_sched_barrier(0);
-      }
-#endif
     }
   };
 
@@ -733,7 +698,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   // the same wave:
   //   [S, dP of half 0] [S, dP of half 1 | dS of half 0] [dQ of half 0 | dS of half 1] [dQ of half 1]
   auto tile_pipe = [&](const char* K, const char* V) {
-    constexpr int L = FA2_DQ_PIPE_LEAD;  // two score pairs live: one step of fragments in flight
+    constexpr int L = kDqPipeLead;  // two score pairs live: one step of fragments in flight
     f32x16 s[2], dp[2];
     u32x4 dsp[2][2];
     // dS of element e (0..15) of half t -> packed pair in dsp[t]
@@ -801,7 +766,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     if (!dead) {
       if (need_mask)
         tile(std::true_type{}, kt(cur), vt(cur), n0);
-      else if constexpr (!BIAS && !DROPOUT && FA2_DQ_PIPE)
+      else if constexpr (!BIAS && !DROPOUT)
         tile_pipe(kt(cur), vt(cur));
       else
         tile(std::false_type{}, kt(cur), vt(cur), n0);
@@ -989,7 +954,7 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
 #pragma unroll
     for (int t = 0; t < HB; ++t) {
       // wave-uniform: no query tile of the wave has this chunk
-      if ((FA2_DS_ABL & 2) || n0 + 32 * t >= nw_max) break;
+      if (n0 + 32 * t >= nw_max) break;
       constexpr int N = 2 * NDT;
       u32x4 fa[N];
 #pragma unroll
@@ -1037,6 +1002,13 @@ __global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd
 }
 
 // ---------------------------------------------------------------------------------------------
+template <bool BF16>
+static void launch_dkv_reduce(const fa2_bwd_args& a, int nsplit, hipStream_t st) {
+  if (nsplit <= 1) return;
+  const int64_t n = (int64_t)a.batch * a.heads_kv * a.seqlen_k * ((a.head_dim + 3) / 4);
+  hipLaunchKernelGGL((dkv_reduce_kernel<BF16>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, nsplit);
+}
+
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
   if constexpr (ALIGNED && DT == 128) {  // head dims 72..128 (fa2_bwd_ds_workspace_bytes)
@@ -1047,13 +1019,10 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
         hipLaunchKernelGGL((delta_kernel<BF16, true>), grid, dim3(256), 0, st, a);
       }
       if ((stages & 2) && a.seqlen_k > 0) {
-        if (FA2_DKDV_PIPE && !BIAS && !DROPOUT) {
-          const hipError_t e = launch_dkdv_pipe<BF16>(a, true, st);
-          if (e != hipSuccess) return e;
-        } else {
-          dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-          hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a);
-        }
+        const int ns = dkv_split(a);
+        dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
+        hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a, ns);
+        launch_dkv_reduce<BF16>(a, ns, st);
       }
       if ((stages & 4) && a.seqlen_q > 0) {
         constexpr int BM = kDqDsWaves * 32 * DqDsQT<CAUSAL>::value;
@@ -1083,9 +1052,10 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
   if ((stages & 2) && a.seqlen_k > 0) {
-    if (FA2_DKDV_PIPE && DT == 128 && ALIGNED && !BIAS && !DROPOUT) return launch_dkdv_pipe<BF16>(a, false, st);
-    dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a);
+    const int ns = dkv_split(a);
+    dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a, ns);
+    launch_dkv_reduce<BF16>(a, ns, st);
   }
   return hipGetLastError();
 }

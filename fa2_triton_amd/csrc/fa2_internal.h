@@ -15,11 +15,6 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st);
 template <bool BF16, int DT>
 hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStream_t st);
 
-// One-wave-per-SIMD software-pipelined dK/dV (dkdv_pipe_kernel.h; head-dim tile 128, aligned,
-// no bias, no dropout); dsout: also store the rounded dS tiles (dS-workspace path).
-template <bool BF16>
-hipError_t launch_dkdv_pipe(const fa2_bwd_args& a, bool dsout, hipStream_t st);
-
 hipError_t launch_cu_seqlens(const uint8_t* mask, int64_t stride, int batch, int seqlen,
                              int32_t* out, hipStream_t st);
 
@@ -50,5 +45,27 @@ struct DsLayout {
   }
   __host__ __device__ int64_t per_head() const { return prefix(nqt); }
 };
+
+// q-head split of dK/dV (ABI 4): the smallest divisor s of the GQA group size G = Hq / Hkv with
+// s * B * Hkv * ceil(Sk / 128) >= kDkvTargetGrid workgroups (two per CU), G if none is; 1 when
+// G == 1 or the grid is already that large.
+constexpr int kDkvTargetGrid = 512;
+inline int dkv_split_count(int B, int Hq, int Hkv, int Sk) {
+  if (B < 1 || Hkv < 1 || Hq % Hkv != 0 || Sk < 1) return 1;
+  const int G = Hq / Hkv;
+  const int64_t grid = (int64_t)((Sk + 127) / 128) * B * Hkv;
+  if (G <= 1 || grid >= kDkvTargetGrid) return 1;
+  for (int s = 2; s < G; ++s)
+    if (G % s == 0 && grid * s >= kDkvTargetGrid) return s;
+  return G;
+}
+inline int64_t dkv_workspace_bytes(int B, int Hq, int Hkv, int Sk, int D) {
+  const int s = dkv_split_count(B, Hq, Hkv, Sk);
+  return s > 1 ? 2 * (int64_t)s * B * Hkv * Sk * D * 4 : 0;
+}
+// the split a launch uses: only with a large enough workspace (checked by fa2_bwd_stages)
+inline int dkv_split(const fa2_bwd_args& a) {
+  return a.dkv_workspace ? dkv_split_count(a.batch, a.heads_q, a.heads_kv, a.seqlen_k) : 1;
+}
 
 }  // namespace fa2

@@ -24,7 +24,6 @@
 #include "common.h"
 #include "fa2_internal.h"
 #include "fwd_pipe_kernel.h"
-#include "fwd_w64_kernel.h"
 
 namespace fa2 {
 
@@ -40,9 +39,6 @@ struct FwdCfg {
 };
 
 
-#ifndef FA2_FWD_W64
-#define FA2_FWD_W64 0  // experimental one-wave-per-SIMD forward (fwd_w64_kernel.h)
-#endif
 #ifndef FA2_OLD_LEAD
 #define FA2_OLD_LEAD 3  // fragment reads in flight ahead of their MFMA (0: compiler order)
 #endif
@@ -403,18 +399,11 @@ static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
 template <bool BF16, int DT>
 hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
-#if FA2_FWD_PIPE
-  // hot path: software-pipelined kernel (fwd_pipe_kernel.h); FA2_FWD_PIPE=1 causal only, 2 both
+  // hot path: software-pipelined kernel (fwd_pipe_kernel.h)
   if constexpr (DT == 64 || DT == 128) {
-    if (aligned && !bi && !dr && a.k_stride[1] == a.v_stride[1] && (c || FA2_FWD_PIPE >= 2))
+    if (aligned && !bi && !dr && a.k_stride[1] == a.v_stride[1])
       return c ? launch_fwd_pipe<BF16, DT, true>(a, st) : launch_fwd_pipe<BF16, DT, false>(a, st);
   }
-#endif
-#if FA2_FWD_W64
-  if constexpr (DT == 64 || DT == 128) {
-    if (aligned && !bi && !dr) return c ? launch_fwd_w64<BF16, DT, true>(a, st) : launch_fwd_w64<BF16, DT, false>(a, st);
-  }
-#endif
 #define FA2_FWD_CASE(C, B, R, A)                                  \
   if (c == C && bi == B && dr == R && aligned == A)               \
     return launch_fwd_t<BF16, DT, C, B, R, A>(a, st);

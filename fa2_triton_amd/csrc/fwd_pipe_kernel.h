@@ -24,10 +24,6 @@
 
 namespace fa2 {
 
-#ifndef FA2_FWD_PIPE
-#define FA2_FWD_PIPE 2
-#endif
-
 #ifndef FA2_FWD_PP
 #define FA2_FWD_PP 0  // ping-pong schedule: 0 never, 1 non-causal only, 2 always
 #endif
@@ -374,9 +370,6 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   };
   using T = std::true_type;
   using F = std::false_type;
-#ifdef FA2_EXP_PRIO
-  if (PP && g == 1) __builtin_amdgcn_s_setprio(1);
-#endif
   int i = 0;
   for (; i + 1 < n_steady; i += 2) {
     step(i, s, s2, T{}, F{});

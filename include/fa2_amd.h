@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 3
+#define FA2_ABI_VERSION 4
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -120,6 +120,15 @@ typedef struct fa2_bwd_args {
    * dims (the reference returns no bias gradient, /root/reference/src/wrapper.py:86). */
   float* dbias;
   int64_t dbias_stride[3];
+  /* optional dK/dV split workspace (ABI 4): when non-NULL and at least
+   * fa2_bwd_dkv_workspace_bytes(args) bytes (> 0 only for GQA / MQA problems whose
+   * B * Hkv * ceil(Sk / 128) key blocks are too few to fill the GPU), the q-heads of each GQA
+   * group are split over several dK/dV workgroups that write fp32 partial sums here, and a
+   * reduction kernel adds them in a fixed order (bitwise reproducible).  NULL: one workgroup
+   * per key block sums the whole group (the reference launches per q-head and sums on the
+   * host, /root/reference/src/backward/caller.py:118-121,162-165).  Contents are scratch. */
+  float* dkv_workspace;
+  int64_t dkv_workspace_bytes;
 } fa2_bwd_args;
 
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
@@ -139,6 +148,11 @@ int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
  * workspace the launch order is bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and
  * fa2_bwd runs all three. */
 int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* args);
+/* Bytes of dK/dV split workspace for these sizes (batch, heads_q, heads_kv, seqlen_k, head_dim):
+ * 2 * nsplit * B * Hkv * Sk * D * 4, with nsplit the smallest divisor of the group size Hq / Hkv
+ * that gives at least 512 dK/dV workgroups (two per CU), or 0 when no split applies (Hq == Hkv,
+ * or the grid is already that large). */
+int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* args);
 
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,
  * row stride mask_row_stride bytes).  Replaces attention_mask.sum(1).cumsum(0) and the

