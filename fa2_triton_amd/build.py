@@ -16,7 +16,9 @@ CSRC = os.path.join(HERE, "csrc")
 GEN = os.path.join(CSRC, "gen")
 OBJ = os.environ.get("FA2_BUILD_DIR", os.path.join(HERE, "_build"))
 LIB = os.environ.get("FA2_LIB_OUT", os.path.join(HERE, "libfa2_amd.so"))
-INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+# the C ABI header: the repo's include/, or a copy inside the package (scripts/export_to_liger.py)
+INCLUDE = next((d for d in (os.path.join(HERE, "include"), os.path.join(os.path.dirname(HERE), "include"))
+                if os.path.exists(os.path.join(d, "fa2_amd.h"))), os.path.join(os.path.dirname(HERE), "include"))
 ARCH = os.environ.get("FA2_OFFLOAD_ARCH", "gfx950")
 
 DTYPES = {"bf16": "true", "f16": "false"}

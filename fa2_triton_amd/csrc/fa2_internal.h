@@ -2,7 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "../../include/fa2_amd.h"
+#include "fa2_amd.h"  // include/ (build.py passes -I)
 
 namespace fa2 {
 

@@ -1,0 +1,54 @@
+"""Package the operator as Liger-Kernel's `liger_kernel.ops.flash_attention`.
+
+The reference ships its Triton sources into a Liger-Kernel checkout the same way
+(/root/reference/export_to_liger.py:6-34: copy src/** except other_implementations/ to
+src/liger_kernel/ops/flash_attention/, rewriting `from src.` imports).  Here the package already
+uses relative imports, so nothing is rewritten; what is copied is the Python host layer, the HIP
+sources with their build script, the C ABI header (into the package's include/, where build.py
+finds it) and the built gfx950 library when present -- the oracle and tests stay behind.
+
+usage: python scripts/export_to_liger.py LIGER_CHECKOUT [--no-lib]
+then:  import liger_kernel.ops.flash_attention as fa; fa.flash_attn_func(q, k, v, causal=True)
+       (rebuild in place with `python -m liger_kernel.ops.flash_attention.build` if needed)
+"""
+import argparse
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "fa2_triton_amd")
+FA_DIR_IN_LIGER = os.path.join("src", "liger_kernel", "ops", "flash_attention")
+
+
+def export(liger_root: str, with_lib: bool = True) -> list:
+    dst = os.path.join(liger_root, FA_DIR_IN_LIGER)
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    os.makedirs(os.path.join(dst, "csrc"))
+    os.makedirs(os.path.join(dst, "include"))
+    written = []
+    for name in sorted(os.listdir(PKG)):
+        if name.endswith(".py") or (with_lib and name == "libfa2_amd.so"):
+            shutil.copy2(os.path.join(PKG, name), os.path.join(dst, name))
+            written.append(os.path.join(dst, name))
+    for name in sorted(os.listdir(os.path.join(PKG, "csrc"))):
+        if name.endswith((".h", ".hip")):  # generated per-instantiation units are rebuilt by build.py
+            shutil.copy2(os.path.join(PKG, "csrc", name), os.path.join(dst, "csrc", name))
+            written.append(os.path.join(dst, "csrc", name))
+    shutil.copy2(os.path.join(ROOT, "include", "fa2_amd.h"), os.path.join(dst, "include", "fa2_amd.h"))
+    written.append(os.path.join(dst, "include", "fa2_amd.h"))
+    return written
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("liger_root")
+    ap.add_argument("--no-lib", action="store_true", help="do not copy the built libfa2_amd.so")
+    args = ap.parse_args(argv)
+    for path in export(args.liger_root, not args.no_lib):
+        print(path)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,34 @@
+"""Liger-style packaging (/root/reference/export_to_liger.py:6-34).
+
+The exported `liger_kernel.ops.flash_attention` must import on its own (relative imports, the
+library next to it), expose the reference's entry points, and bind the same C ABI.
+"""
+import importlib
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_export_imports_as_liger_op(tmp_path):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "export_to_liger.py"), str(tmp_path)],
+                         capture_output=True, text=True, check=True).stdout.split()
+    dst = tmp_path / "src" / "liger_kernel" / "ops" / "flash_attention"
+    assert str(dst / "wrapper.py") in out and (dst / "include" / "fa2_amd.h").exists()
+    assert (dst / "csrc" / "bwd_kernel.h").exists() and (dst / "build.py").exists()
+    assert not any("oracle" in p or "tests" in p for p in out)
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import liger_kernel.ops.flash_attention as fa\n"
+        "from liger_kernel.ops.flash_attention import _lib\n"
+        "assert callable(fa.flash_attn_func) and fa.FlashAttnFunc.apply\n"
+        "assert _lib.LIB_PATH.startswith(%r)\n"
+        "lib = _lib.load(); [getattr(lib, s) for s in _lib.EXPORTED_SYMBOLS]\n"
+        "from liger_kernel.ops.flash_attention import build\n"
+        "assert build.INCLUDE == %r\n"
+        "print('ok')\n" % (str(tmp_path / "src"), str(dst), str(dst / "include"))
+    )
+    env = {k: v for k, v in os.environ.items() if k != "FA2_AMD_LIB"}
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=str(tmp_path))
+    assert res.returncode == 0 and "ok" in res.stdout, res.stderr
