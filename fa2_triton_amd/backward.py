@@ -47,12 +47,16 @@ def ds_workspace_bytes(q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, c
 
 
 def _ds_workspace_cap(device: torch.device) -> int:
-    """Largest dS workspace the backward allocates by itself: FA2_DS_WORKSPACE_MAX_GB if set (0
-    disables the dS path), otherwise half of the memory available right now -- free device
-    memory plus what torch's caching allocator holds unused -- so that the O(S^2) workspace never
-    takes memory the rest of a training step needs (B=8 H=32 S=4096 causal needs 4.33 GB)."""
+    """Largest dS workspace the backward allocates by itself.  The dS path is opt-in: with the
+    software-pipelined dK/dV kernel the recompute path is as fast or faster (cfg3 causal bwd
+    3.73 vs 3.85 ms, non-causal 6.51 vs 6.49 ms, profiles/r02_ab_bwd_paths.txt) and needs O(S)
+    memory, as the reference's backward.  FA2_DS_WORKSPACE_MAX_GB=<GB> enables it under that cap
+    (0 disables), =auto under half of the memory available right now (free device memory plus
+    what torch's caching allocator holds unused)."""
     env = os.environ.get("FA2_DS_WORKSPACE_MAX_GB")
-    if env is not None:
+    if env is None:
+        return 0
+    if env.strip().lower() != "auto":
         return int(float(env) * (1 << 30))
     free, _ = torch.cuda.mem_get_info(device)
     cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)

@@ -28,6 +28,15 @@
 // The dS workspace is written with non-temporal stores (1.5 % faster dK/dV than plain stores;
 // sc1 / sc0 sc1 / sc1 nt: +38 %, +38 %, +75 %) and read with nt LDS-DMA (a once-read stream).
 #define FA2_DS_LD_POLICY "nt "
+#ifndef FA2_DKDV_VOFF_RECOMPUTE
+#define FA2_DKDV_VOFF_RECOMPUTE 0
+#endif
+#ifndef FA2_DKDV_DS_EARLY
+#define FA2_DKDV_DS_EARLY 1
+#endif
+#ifndef FA2_DKDV_PIPE_DS
+#define FA2_DKDV_PIPE_DS 0
+#endif
 
 namespace fa2 {
 
@@ -58,7 +67,8 @@ struct DqDsQT {  // dq_ds_kernel: 32-query tiles per wave
 constexpr int kDqDsStages = FA2_DQDS_STAGES;  // dq_ds_kernel: ring of K + dS tiles in LDS
 
 // ---------------------------------------------------------------------------------------------
-// delta[b, h, i] = sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows)
+// delta[b, h, i] = -sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows).  The
+// workspace holds the NEGATED row sum: it is the initial dP accumulator of dkdv_kernel.
 template <bool BF16, bool ALIGNED>
 __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
@@ -88,7 +98,8 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, LPR);
   // rows [Lq, lse_row_stride) get 0 so that masked rows can never inject NaN/Inf garbage
-  if (sub == 0 && row < p.lse_row_stride) p.delta[(int64_t)bh * p.lse_row_stride + row] = acc;
+  // stored negated: the dK/dV kernel starts its dP accumulator at -delta
+  if (sub == 0 && row < p.lse_row_stride) p.delta[(int64_t)bh * p.lse_row_stride + row] = -acc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -175,17 +186,40 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
     const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
-    if constexpr (ALIGNED) {
+    if constexpr (ALIGNED && !FA2_DKDV_VOFF_RECOMPUTE) {
       qst.issue(qt(buf), qg, p.q_stride[1], m, Lq, qrows);
       ost.issue(ot(buf), og, p.do_stride[1], m, Lq, orows);
+    } else if constexpr (ALIGNED) {
+      // lane offsets recomputed from an opaque thread id each step (BufStager::voff_at)
+      int t = threadIdx.x;
+      asm volatile("" : "+v"(t));
+      using QS = BufStager<DT, BMQ, NT>;
+      const i32x4 rq = QS::tile_rsrc(qg, p.q_stride[1], m, Lq, qrows);
+      const i32x4 ro = QS::tile_rsrc(og, p.do_stride[1], m, Lq, orows);
+      if (D == DT) {  // one offset register per tile, the pieces at immediate offsets
+        const uint32_t q0 = QS::voff_at(t, 0, p.q_stride[1], DT), o0 = QS::voff_at(t, 0, p.do_stride[1], DT);
+        static_for<QS::kIters>([&](auto it) { qst.template piece_imm<decltype(it)::value>(qt(buf), rq, q0); });
+        static_for<QS::kIters>([&](auto it) { ost.template piece_imm<decltype(it)::value>(ot(buf), ro, o0); });
+      } else {
+#pragma unroll
+        for (int it = 0; it < QS::kIters; ++it) qst.piece_at(qt(buf), rq, it, QS::voff_at(t, it, p.q_stride[1], D));
+#pragma unroll
+        for (int it = 0; it < QS::kIters; ++it) ost.piece_at(ot(buf), ro, it, QS::voff_at(t, it, p.do_stride[1], D));
+      }
     } else {
       stage_tile<DT, BMQ, NT, false>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
       stage_tile<DT, BMQ, NT, false>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
     }
     if (w == 0) {  // LSE2 rows -> lanes 0..31, delta rows -> lanes 32..63 (one 256-byte piece)
-      const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m + r32;
-      const float* src = hh ? p.delta + srow : p.lse + srow;
-      glds4(src, __builtin_amdgcn_readfirstlane(lds_addr(st(buf))));
+      // wave-uniform row bases in SGPR descriptors (no per-lane 64-bit address at the register
+      // limit); each half-wave issues the piece of its own array
+      const int64_t row0 = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m;
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf)));
+      int t = threadIdx.x;
+      asm volatile("" : "+v"(t));
+      const uint32_t voff = (uint32_t)(t & 31) * 4u;
+      if (((t >> 5) & 1) == 0) blds4(voff, make_rsrc(p.lse + row0, BMQ * 4), lds);
+      else blds4(voff, make_rsrc(p.delta + row0, BMQ * 4), lds);
     }
   };
 
@@ -256,8 +290,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       const int kl = n0 + 32 * (ln >> 6) + (ln & 31);
       const int qlo = CAUSAL ? max(kl - diag, 0) : 0;
       const int qhi = kl < Lk ? Lq : -1;
-      lo = qlo - m - 4 * hh;
-      hi = qhi - m - 4 * hh;
+      lo = qlo - m - 4 * ((ln >> 5) & 1);  // (hh, likewise from the opaque id)
+      hi = qhi - m - 4 * ((ln >> 5) & 1);
     }
     u32x4 pp[2], dsp[2];
     auto store_ds = [&]() {
@@ -297,10 +331,10 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
           const bool keep = philox_uniform(p.dropout_seed, drop_base(hq) + qr * (uint64_t)Lk + (uint64_t)kj) > p.dropout_p;
           const float kp = keep ? inv_keep : 0.f;
           pv[j] = pr * kp;
-          dsv[j] = pr * (dp[i] * kp - d4[j]);
+          dsv[j] = pr * (dp[i] * kp + d4[j]);  // d4 = -delta (workspace convention)
         } else {
           pv[j] = pr;
-          dsv[j] = pr * (dp[i] - d4[j]);  // softmax_scale is applied to dK once, at the end
+          dsv[j] = pr * (dp[i] + d4[j]);  // softmax_scale is applied to dK once, at the end
         }
         if constexpr (BIAS) {
           // bias gradient dL/ds_ij = dS (fp32, before rounding): one element per register
@@ -340,6 +374,138 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
   };
 
+  // The plain step (no bias, no dropout), software-pipelined inside the wave so that the
+  // softmax-gradient VALU work sits beside MFMAs of the same wave instead of in a VALU-only phase:
+  //   [S chain] [dP chain | P = exp2(S sc - LSE2)] [dV, dK chains | dS = P dP', packs, dS stores]
+  // The dP accumulator starts at -delta (the delta workspace holds -rowsum(O dO)), so the chain
+  // yields dP - delta and dS is one multiply; the LSE2 and -delta rows are read from LDS at the
+  // start of the step, long before their use.
+  auto body_pipe = [&](auto mask_c, const char* Q, const char* O, const char* S, int m) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    constexpr int LS = kDkdvLS < KS ? kDkdvLS : KS, LD = kDkdvLD < KS ? kDkdvLD : KS;
+    constexpr int EP = 16 / KS;          // P elements per dP step
+    constexpr int N = 4 * NDT;           // dV / dK steps
+    constexpr int ED = 8 / NDT;          // dS elements per dV / dK step (first 2 NDT steps)
+    constexpr int LT = 2 < N ? 2 : N;    // transposed fragments in flight
+    f32x16 s, dp;
+    f32x4 l4[4];  // LSE2 rows of register group g4 (rows 8 g4 + 4 hh + 0..3), read just ahead
+    auto rd_lse = [&](int g4) { l4[g4] = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh)); };
+    auto rd_nd = [&](int g4) {  // -delta rows of group g4 into the dP accumulator
+      const f32x4 d4 = *(const f32x4*)(S + 4 * BMQ + 4 * (8 * g4 + 4 * hh));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dp[4 * g4 + j] = d4[j];
+    };
+    u32x4 fq[KS], fo[KS], fv[KS];
+#pragma unroll
+    for (int j = 0; j < LS; ++j) fq[j] = lds_row_frag<DT, BMQ>(Q, 0, r32, j, hh);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + LS < KS) fq[ks + LS] = lds_row_frag<DT, BMQ>(Q, 0, r32, ks + LS, hh);
+      if (ks + LD >= KS) {
+        const int j = ks + LD - KS;
+        fo[j] = lds_row_frag<DT, BMQ>(O, 0, r32, j, hh);
+        fv[j] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, j, hh);
+      }
+      // the -delta rows land in the dP accumulator over the last S steps, LSE group 0 last
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        if ((KS >= 4 ? ks == KS - 4 + g4 : ks == KS - 2 + g4 / 2)) rd_nd(g4);
+      // LSE group g4 is first used at dP step 4 g4 / EP and read one step ahead; the groups
+      // needed in dP step 0 are read here
+      if (ks == KS - 1) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          if ((4 * g4) / EP == 0) rd_lse(g4);
+      }
+      s = E::mfma(fq[ks], kf[ks], ks == 0 ? zero16() : s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int lo = 0, hi = 0;  // as in body(): the visible row window of this lane's key
+    if (MASK) {
+      int ln = threadIdx.x;
+      asm volatile("" : "+v"(ln));
+      const int kl = n0 + 32 * (ln >> 6) + (ln & 31);
+      const int qlo = CAUSAL ? max(kl - diag, 0) : 0;
+      const int qhi = kl < Lk ? Lq : -1;
+      lo = qlo - m - 4 * ((ln >> 5) & 1);  // (hh, likewise from the opaque id)
+      hi = qhi - m - 4 * ((ln >> 5) & 1);
+    }
+    u32x4 pp[2], dsp[2];
+    auto p_elem = [&](int i) {  // P in place of S, packed pairwise
+      const int o = (i & 3) + 8 * (i >> 2);
+      float pr = __builtin_amdgcn_exp2f(fmaf(s[i], sc, -l4[i >> 2][i & 3]));
+      if (MASK) pr = (o >= lo && o < hi) ? pr : 0.f;
+      s[i] = pr;
+    };
+    auto p_pack = [&](int sp) {  // P packed for the dV product, right before its first use
+#pragma unroll
+      for (int t = 0; t < 4; ++t) pp[sp][t] = E::pack2(s[8 * sp + 2 * t], s[8 * sp + 2 * t + 1]);
+    };
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + LD < KS) {
+        fo[ks + LD] = lds_row_frag<DT, BMQ>(O, 0, r32, ks + LD, hh);
+        fv[ks + LD] = lds_row_frag<DT, BNK>(Vs, 32 * w, r32, ks + LD, hh);
+      }
+      dp = E::mfma(fo[ks], fv[ks], dp);
+#pragma unroll
+      for (int e = ks * EP; e < (ks + 1) * EP; ++e) p_elem(e);
+#pragma unroll
+      for (int g4 = 1; g4 < 4; ++g4)
+        if ((4 * g4) / EP > 0 && ks == (4 * g4) / EP - 1) rd_lse(g4);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    auto ds_elem = [&](int i) {  // dS = P (dP - delta) in place of dP, packed pairwise
+      dp[i] = s[i] * dp[i];
+      if (i & 1) dsp[i >> 3][(i & 7) >> 1] = E::pack2(dp[i - 1], dp[i]);
+    };
+    // steps m: dt = m % NDT, r = m / NDT: dV (sp 0), dK (sp 0), dV (sp 1), dK (sp 1); dS elements
+    // 0..7 ride on the first NDT steps, 8..15 on the next NDT (dsp[1] is first read at r = 3)
+    auto store_ds = [&](int which) {
+      // buffer stores: the chunk base is wave-uniform (SGPR descriptor), the lane offset
+      // recomputed -- no address VGPRs live across the loop; which: 1 = dsp[0], 2 = dsp[1]
+      const i32x4 rs = make_rsrc((const char*)p.ds_workspace + ds_chunk * kDsChunk, kDsChunk);
+      int t = threadIdx.x;
+      asm volatile("" : "+v"(t));
+      const uint32_t voff = (uint32_t)((t & 31) * 64 + (t & 32));
+      if (which & 1) asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt" ::"v"(dsp[0]), "v"(voff), "s"(rs) : "memory");
+      if (which & 2) asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:16 nt" ::"v"(dsp[1]), "v"(voff), "s"(rs) : "memory");
+    };
+    constexpr bool DS_EARLY = DSOUT && FA2_DKDV_DS_EARLY;
+    if constexpr (DS_EARLY) {
+      // dS stores as early as possible (measured: their completion time, not their issue cost,
+      // sets the step time): dS computed right after the dP chain
+#pragma unroll
+      for (int e = 0; e < 16; ++e) ds_elem(e);
+      store_ds(3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    u32x4 fr[N];
+    auto rd = [&](int mm) {
+      const int dt = mm % NDT, r = mm / NDT;
+      return lds_tr_frag<DT, BMQ>((r & 1) ? Q : O, 16 * (r >> 1), 32 * dt, lane);
+    };
+#pragma unroll
+    for (int j = 0; j < LT; ++j) fr[j] = rd(j);
+    p_pack(0);
+#pragma unroll
+    for (int mm = 0; mm < N; ++mm) {
+      if (mm + LT < N) fr[mm + LT] = rd(mm + LT);
+      const int dt = mm % NDT, r = mm / NDT;
+      if (mm == 2 * NDT - 1) p_pack(1);  // pp[1] is first read at r = 2
+      if (r & 1) dk[dt] = E::mfma(fr[mm], dsp[r >> 1], dk[dt]);
+      else dv[dt] = E::mfma(fr[mm], pp[r >> 1], dv[dt]);
+      if (!DS_EARLY && mm < 2 * NDT) {
+#pragma unroll
+        for (int e = mm * ED; e < (mm + 1) * ED; ++e) ds_elem(e);
+      }
+      if constexpr (DSOUT && !DS_EARLY) {
+        if (mm == 2 * NDT - 1) store_ds(3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
   __syncthreads();
   if (ALIGNED && D < DT && total > 0) {
@@ -364,10 +530,17 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
     const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);
     if (!dead) {
-      if (need_mask)
-        body(std::true_type{}, qt(cur), ot(cur), st(cur), hq, m);
-      else
-        body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
+      if constexpr (!BIAS && !DROPOUT && (!DSOUT || FA2_DKDV_PIPE_DS)) {
+        if (need_mask)
+          body_pipe(std::true_type{}, qt(cur), ot(cur), st(cur), m);
+        else
+          body_pipe(std::false_type{}, qt(cur), ot(cur), st(cur), m);
+      } else {
+        if (need_mask)
+          body(std::true_type{}, qt(cur), ot(cur), st(cur), hq, m);
+        else
+          body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
+      }
     }
     if constexpr (DSOUT) {
       // the 2 dS stores of this step were issued after the next tile's LDS-DMA: wait for all
@@ -384,9 +557,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     if (++mt == n_mt) {
       mt = 0;
       ++g;
-      if constexpr (DSOUT) ds_chunk = ds_head += L.per_head();
+      if constexpr (DSOUT) ds_chunk = ds_head = uniform64(ds_head + L.per_head());
     } else if constexpr (DSOUT) {
-      ds_chunk += min(max((m >> 5) + L.c, 0), L.nkt);  // nvis of the q-tile left behind
+      ds_chunk = uniform64(ds_chunk + min(max((m >> 5) + L.c, 0), L.nkt));  // nvis of the q-tile left behind
     }
   }
 
@@ -596,7 +769,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
       }
     }
     del_i = qvalid ? half_sum(part) : 0.f;
-    if (hh == 0 && qi < p.lse_row_stride) p.delta[srow + qi] = del_i;
+    if (hh == 0 && qi < p.lse_row_stride) p.delta[srow + qi] = -del_i;  // negated (delta_kernel)
   }
 
   f32x16 acc[NDT];

@@ -81,7 +81,7 @@ typedef struct fa2_bwd_args {
   const void* o;
   const void* dout;       /* dO, [B, Sq, Hq, D] */
   const float* lse;       /* as written by fa2_fwd */
-  float* delta;           /* workspace [B, Hq, lse_row_stride] fp32 (rowsum(O * dO)) */
+  float* delta;           /* workspace [B, Hq, lse_row_stride] fp32: -rowsum(O * dO) (scratch) */
   void* dq;               /* [B, Sq, Hq, D] in dq_dtype */
   void* dk;               /* [B, Sk, Hkv, D] in dtype */
   void* dv;               /* [B, Sk, Hkv, D] in dtype */

@@ -84,9 +84,21 @@ def test_ds_path_fp32_dq():
 @pytest.mark.gpu
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("use_mask", [False, True])
-def test_ds_path_vs_oracle(causal, use_mask):
-    # run_case goes through flash_attn_func, whose backward allocates the workspace itself
+def test_ds_path_vs_oracle(causal, use_mask, monkeypatch):
+    # run_case goes through flash_attn_func, whose backward allocates the workspace itself once
+    # the (opt-in) dS path is enabled
+    monkeypatch.setenv("FA2_DS_WORKSPACE_MAX_GB", "auto")
     run_case(2, 8, 2, 700, 700, 128, causal, 0.0, use_mask, False, torch.bfloat16, False)
+
+
+def test_ds_path_is_opt_in(monkeypatch):
+    """Default backward: the O(S)-memory recompute path (no dS workspace is allocated)."""
+    from fa2_triton_amd.backward import _ds_workspace_cap
+
+    monkeypatch.delenv("FA2_DS_WORKSPACE_MAX_GB", raising=False)
+    assert _ds_workspace_cap(torch.device("cpu")) == 0
+    monkeypatch.setenv("FA2_DS_WORKSPACE_MAX_GB", "1.5")
+    assert _ds_workspace_cap(torch.device("cpu")) == 3 << 29
 
 
 @pytest.mark.gpu
@@ -125,7 +137,7 @@ def test_ds_workspace_capped_by_free_memory(monkeypatch):
     path instead of the dS path -- never an OOM where the reference's backward would run."""
     import fa2_triton_amd.backward as bw
 
-    monkeypatch.delenv("FA2_DS_WORKSPACE_MAX_GB", raising=False)
+    monkeypatch.setenv("FA2_DS_WORKSPACE_MAX_GB", "auto")
     q, k, v, do = generate_test_data(4, 32, 32, 1024, 1024, 128, torch.bfloat16)
     need = ds_workspace_bytes(q, k, v, q, do, True)
     assert need > 100 << 20
