@@ -28,22 +28,29 @@
 // The dS workspace is written with non-temporal stores (1.5 % faster dK/dV than plain stores;
 // sc1 / sc0 sc1 / sc1 nt: +38 %, +38 %, +75 %) and read with nt LDS-DMA (a once-read stream).
 #define FA2_DS_LD_POLICY "nt "
-#ifndef FA2_DKDV_VOFF_RECOMPUTE
-#define FA2_DKDV_VOFF_RECOMPUTE 0
-#endif
-#ifndef FA2_DKDV_DS_EARLY
-#define FA2_DKDV_DS_EARLY 1
-#endif
-#ifndef FA2_DKDV_PIPE_DS
-#define FA2_DKDV_PIPE_DS 0
-#endif
 
 namespace fa2 {
 
-constexpr int kDkdvLS = 2;
-constexpr int kDkdvLD = 1;
-constexpr int kDqLead = 2;
-constexpr int kDqPipeLead = 1;
+#ifndef FA2_DKDV_LS
+#define FA2_DKDV_LS 2
+#endif
+#ifndef FA2_DKDV_LD
+#define FA2_DKDV_LD 1
+#endif
+#ifndef FA2_DKDV_LT
+#define FA2_DKDV_LT 2
+#endif
+constexpr int kDkdvLS = FA2_DKDV_LS;
+constexpr int kDkdvLD = FA2_DKDV_LD;
+constexpr int kDkdvLT = FA2_DKDV_LT;
+#ifndef FA2_DQ_LEAD
+#define FA2_DQ_LEAD 2
+#endif
+#ifndef FA2_DQ_PIPE_LEAD
+#define FA2_DQ_PIPE_LEAD 1
+#endif
+constexpr int kDqLead = FA2_DQ_LEAD;
+constexpr int kDqPipeLead = FA2_DQ_PIPE_LEAD;
 
 constexpr int kDsChunk = 32 * 32 * 2;  // bytes of one 32-key x 32-query dS tile in the workspace
 constexpr int kDqDsWaves = 8;          // dq_ds_kernel: waves (32 query rows each) per workgroup
@@ -186,26 +193,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
     const uint16_t* qg = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2];
     const uint16_t* og = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2];
-    if constexpr (ALIGNED && !FA2_DKDV_VOFF_RECOMPUTE) {
+    if constexpr (ALIGNED) {
       qst.issue(qt(buf), qg, p.q_stride[1], m, Lq, qrows);
       ost.issue(ot(buf), og, p.do_stride[1], m, Lq, orows);
-    } else if constexpr (ALIGNED) {
-      // lane offsets recomputed from an opaque thread id each step (BufStager::voff_at)
-      int t = threadIdx.x;
-      asm volatile("" : "+v"(t));
-      using QS = BufStager<DT, BMQ, NT>;
-      const i32x4 rq = QS::tile_rsrc(qg, p.q_stride[1], m, Lq, qrows);
-      const i32x4 ro = QS::tile_rsrc(og, p.do_stride[1], m, Lq, orows);
-      if (D == DT) {  // one offset register per tile, the pieces at immediate offsets
-        const uint32_t q0 = QS::voff_at(t, 0, p.q_stride[1], DT), o0 = QS::voff_at(t, 0, p.do_stride[1], DT);
-        static_for<QS::kIters>([&](auto it) { qst.template piece_imm<decltype(it)::value>(qt(buf), rq, q0); });
-        static_for<QS::kIters>([&](auto it) { ost.template piece_imm<decltype(it)::value>(ot(buf), ro, o0); });
-      } else {
-#pragma unroll
-        for (int it = 0; it < QS::kIters; ++it) qst.piece_at(qt(buf), rq, it, QS::voff_at(t, it, p.q_stride[1], D));
-#pragma unroll
-        for (int it = 0; it < QS::kIters; ++it) ost.piece_at(ot(buf), ro, it, QS::voff_at(t, it, p.do_stride[1], D));
-      }
     } else {
       stage_tile<DT, BMQ, NT, false>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
       stage_tile<DT, BMQ, NT, false>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
@@ -379,14 +369,15 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   //   [S chain] [dP chain | P = exp2(S sc - LSE2)] [dV, dK chains | dS = P dP', packs, dS stores]
   // The dP accumulator starts at -delta (the delta workspace holds -rowsum(O dO)), so the chain
   // yields dP - delta and dS is one multiply; the LSE2 and -delta rows are read from LDS at the
-  // start of the step, long before their use.
+  // start of the step, long before their use.  (The dS-workspace path keeps `body`: with its dS
+  // stores issued inside the dV/dK chain this schedule measured 1-13 % slower there, DESIGN.md.)
   auto body_pipe = [&](auto mask_c, const char* Q, const char* O, const char* S, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     constexpr int LS = kDkdvLS < KS ? kDkdvLS : KS, LD = kDkdvLD < KS ? kDkdvLD : KS;
     constexpr int EP = 16 / KS;          // P elements per dP step
     constexpr int N = 4 * NDT;           // dV / dK steps
     constexpr int ED = 8 / NDT;          // dS elements per dV / dK step (first 2 NDT steps)
-    constexpr int LT = 2 < N ? 2 : N;    // transposed fragments in flight
+    constexpr int LT = kDkdvLT < N ? kDkdvLT : N;  // transposed fragments in flight
     f32x16 s, dp;
     f32x4 l4[4];  // LSE2 rows of register group g4 (rows 8 g4 + 4 hh + 0..3), read just ahead
     auto rd_lse = [&](int g4) { l4[g4] = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh)); };
@@ -461,25 +452,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     };
     // steps m: dt = m % NDT, r = m / NDT: dV (sp 0), dK (sp 0), dV (sp 1), dK (sp 1); dS elements
     // 0..7 ride on the first NDT steps, 8..15 on the next NDT (dsp[1] is first read at r = 3)
-    auto store_ds = [&](int which) {
-      // buffer stores: the chunk base is wave-uniform (SGPR descriptor), the lane offset
-      // recomputed -- no address VGPRs live across the loop; which: 1 = dsp[0], 2 = dsp[1]
-      const i32x4 rs = make_rsrc((const char*)p.ds_workspace + ds_chunk * kDsChunk, kDsChunk);
-      int t = threadIdx.x;
-      asm volatile("" : "+v"(t));
-      const uint32_t voff = (uint32_t)((t & 31) * 64 + (t & 32));
-      if (which & 1) asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen nt" ::"v"(dsp[0]), "v"(voff), "s"(rs) : "memory");
-      if (which & 2) asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:16 nt" ::"v"(dsp[1]), "v"(voff), "s"(rs) : "memory");
-    };
-    constexpr bool DS_EARLY = DSOUT && FA2_DKDV_DS_EARLY;
-    if constexpr (DS_EARLY) {
-      // dS stores as early as possible (measured: their completion time, not their issue cost,
-      // sets the step time): dS computed right after the dP chain
-#pragma unroll
-      for (int e = 0; e < 16; ++e) ds_elem(e);
-      store_ds(3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     u32x4 fr[N];
     auto rd = [&](int mm) {
       const int dt = mm % NDT, r = mm / NDT;
@@ -495,12 +467,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       if (mm == 2 * NDT - 1) p_pack(1);  // pp[1] is first read at r = 2
       if (r & 1) dk[dt] = E::mfma(fr[mm], dsp[r >> 1], dk[dt]);
       else dv[dt] = E::mfma(fr[mm], pp[r >> 1], dv[dt]);
-      if (!DS_EARLY && mm < 2 * NDT) {
+      if (mm < 2 * NDT) {
 #pragma unroll
         for (int e = mm * ED; e < (mm + 1) * ED; ++e) ds_elem(e);
-      }
-      if constexpr (DSOUT && !DS_EARLY) {
-        if (mm == 2 * NDT - 1) store_ds(3);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -530,7 +499,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
     const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);
     if (!dead) {
-      if constexpr (!BIAS && !DROPOUT && (!DSOUT || FA2_DKDV_PIPE_DS)) {
+      if constexpr (!BIAS && !DROPOUT && !DSOUT) {
         if (need_mask)
           body_pipe(std::true_type{}, qt(cur), ot(cur), st(cur), m);
         else

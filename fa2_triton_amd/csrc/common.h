@@ -201,17 +201,6 @@ FA2_DEV int64_t uniform64(int64_t x) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
-template <int I, int N, typename F>
-FA2_DEV void static_for_impl(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for_impl<I + 1, N>(f);
-  }
-}
-template <int N, typename F>
-FA2_DEV void static_for(F&& f) { static_for_impl<0, N>(f); }
-
 FA2_DEV void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
@@ -383,42 +372,6 @@ struct BufStager {
       // 64-bit products here get kept as register pairs, which kernels at the register limit spill
       voff[it] = ((uint32_t)pr * (uint32_t)row_stride + (uint32_t)(gc * 8)) * 2u;
     }
-  }
-  // The byte offset of piece `it` of thread `tid` (what init() stores in voff[it]).  Kernels at
-  // the register limit compute it per tile from an opaque thread id instead of keeping the
-  // offsets live across their loop: the allocator spills loop-invariant lane values there, and
-  // each scratch reload's vmcnt(0) would drain the LDS-DMA and stores in flight.
-  FA2_DEV static uint32_t voff_at(int tid, int it, int64_t row_stride, int D) {
-    const int piece = it * NTHREADS + tid;
-    const int sub = piece / (ROWS * 4), within = piece % (ROWS * 4);
-    const int pr = within >> 2;
-    const int c = sub * 4 + ((within & 3) ^ ((pr >> 2) & 3));
-    const int gc = c < (D >> 3) ? c : (D >> 3) - 1;
-    return ((uint32_t)pr * (uint32_t)row_stride + (uint32_t)(gc * 8)) * 2u;
-  }
-  // piece `it` at voff_at(tid, 0, ...) + it * kItBytes: valid when D == DT (no column clamp)
-  // and NTHREADS % (ROWS * 4) == 0, so one offset register serves all pieces (immediates)
-  static constexpr uint32_t kItBytes = (uint32_t)(NTHREADS / (ROWS * 4)) * 64u;
-  template <int IT>
-  FA2_DEV void piece_imm(char* tile, i32x4 rsrc, uint32_t off0) const {
-    static_assert(NTHREADS % (ROWS * 4) == 0 && IT * kItBytes < 4096, "immediate offset");
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds + IT * NTHREADS * 16;
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen offset:%4 lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(off0), "s"(rsrc), "s"(lds), "i"(IT * kItBytes)
-        : "memory");
-  }
-  FA2_DEV void piece_at(char* tile, i32x4 rsrc, int it, uint32_t off) const {
-    if (kPieces % NTHREADS != 0 && wave * 64 >= kPieces) return;  // small tile: idle waves
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds + it * NTHREADS * 16;
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(off), "s"(rsrc), "s"(lds)
-        : "memory");
   }
   // descriptor of the tile starting at row row0 of g (rows >= row_end read as zero)
   // (max_rows = rows whose bytes fit the 32-bit range field, see max_rows())
