@@ -568,6 +568,15 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
     return;
   }
+  if constexpr (FA2_STORE_LDS && ALIGNED) {
+    // every wave passed the last step's barrier: V and Q/dO buffers hold the staging images
+    uint16_t* k0 = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kw0 * p.dk_stride[1];
+    uint16_t* v0 = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kw0 * p.dv_stride[1];
+    const int nrows = min(32, p.seqlen_k - kw0);
+    store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, dk, scale, kval, k0, p.dk_stride[1], nrows, D, lane);
+    store_rows_lds<BF16, DT>(smem + (4 + w) * 32 * DT * 2, dv, 1.f, kval, v0, p.dv_stride[1], nrows, D, lane);
+    return;
+  }
   if (kj < p.seqlen_k) {
     uint16_t* dkrow = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kj * p.dk_stride[1];
     uint16_t* dvrow = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kj * p.dv_stride[1];
@@ -917,7 +926,12 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     __syncthreads();
   }
 
-  if (qi < p.seqlen_q) {
+  if constexpr (FA2_STORE_LDS && ALIGNED && !DQF32) {
+    // the last tile's barrier is behind every wave: the K/V buffers hold the staging images
+    uint16_t* q0 = (uint16_t*)p.dq + b * p.dq_stride[0] + hq * p.dq_stride[2] + (int64_t)mw0 * p.dq_stride[1];
+    store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, scale, qvalid, q0, p.dq_stride[1],
+                             min(32, p.seqlen_q - mw0), D, lane);
+  } else if (qi < p.seqlen_q) {
     const bool ok = qvalid;
     char* base = (char*)p.dq;
     const int esz = DQF32 ? 4 : 2;

@@ -39,6 +39,12 @@ constexpr float kNegInf = -__builtin_inff();
 // accumulation and bf16/fp16 P (same relative precision at any magnitude) absorb exactly.
 constexpr float kDeferMax = 8.f;
 
+// Epilogue stores of the aligned bf16/fp16 outputs (O, dQ, dK, dV) through LDS, whole rows per
+// store instruction (store_rows_lds); 0 = row-per-lane stores straight from registers.
+#ifndef FA2_STORE_LDS
+#define FA2_STORE_LDS 1
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Element traits: raw 16-bit storage, conversions and the matching MFMA.
 template <bool BF16>
@@ -414,6 +420,53 @@ FA2_DEV u32x4 load_row_frag(const uint16_t* row, int d0, int D, bool valid) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) pk[j] = uint32_t(v[2 * j]) | (uint32_t(v[2 * j + 1]) << 16);
     return pk;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Epilogue store of one wave's 32 x DT accumulator image through a wave-private LDS staging area.
+// acc[dt] is C^T of a swapped product: lane (r = lane & 31, h = lane >> 5) holds output row r,
+// columns 32 dt + 8 (i >> 2) + 4 h + (i & 3).  Stored straight from registers, every store
+// instruction touches 32 rows x 16 bytes (row-per-lane); the epilogue tail is bound by the number
+// of such row segments, not by bytes (MI355X_MICROARCH.md, "attention epilogue store tail").  Here
+// each lane pair first writes its row into LDS (one ds_write_b128 per 8 columns after a
+// v_permlane32_swap pairing), then the wave reads the image back row-contiguous: instruction j
+// stores rows j * RPI .. j * RPI + RPI - 1 as whole D * 2-byte segments.
+// Staging image: row r at r * DT * 2 bytes, 16-byte chunk c at c ^ (r % CPR) -- conflict free for
+// the 8-lane write groups (8 rows, one chunk) and for the ds_read_b128 lane groups (whole rows).
+// Element value: valid ? acc * mul : 0, rounded once.  Rows [nrows, 32) and columns [D, DT) are
+// not stored (D % 8 == 0).  The caller guarantees no other wave still reads `stage`.
+template <bool BF16, int DT>
+FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool valid, uint16_t* g0, int64_t rstride,
+                            int nrows, int D, int lane) {
+  using E = Elem<BF16>;
+  constexpr int NDT = DT / 32;
+  constexpr int CPR = DT / 8;   // 16-byte chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per store instruction
+  const int r = lane & 31, h = lane >> 5;
+  const float m = valid ? mul : 0.f;
+  char* row = stage + r * (DT * 2);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; g4 += 2) {
+      const uint32_t a0 = E::pack2(acc[dt][4 * g4 + 0] * m, acc[dt][4 * g4 + 1] * m);
+      const uint32_t a1 = E::pack2(acc[dt][4 * g4 + 2] * m, acc[dt][4 * g4 + 3] * m);
+      const uint32_t b0 = E::pack2(acc[dt][4 * g4 + 4] * m, acc[dt][4 * g4 + 5] * m);
+      const uint32_t b1 = E::pack2(acc[dt][4 * g4 + 6] * m, acc[dt][4 * g4 + 7] * m);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      const int c = 4 * dt + g4 + h;  // chunk: columns 8c .. 8c + 7
+      *(u32x4*)(row + 16 * (c ^ (r % CPR))) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int c = lane % CPR;
+#pragma unroll
+  for (int j = 0; j < 32 / RPI; ++j) {
+    const int R = j * RPI + lane / CPR;
+    const u32x4 v = *(const u32x4*)(stage + R * (DT * 2) + 16 * (c ^ (R % CPR)));
+    if (R < nrows && 8 * c < D) *(u32x4*)(g0 + (int64_t)R * rstride + 8 * c) = v;
   }
 }
 

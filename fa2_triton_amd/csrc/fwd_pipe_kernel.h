@@ -426,7 +426,12 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   // v_permlane32_swap per dword pairs groups k, k+1 so that each lane stores 16 contiguous
   // bytes (lanes 0-31: columns 8k..8k+7, lanes 32-63: 8k+8..8k+15): 8 dwordx4 stores instead
   // of 16 dwordx2 (the store tail is issue-bound).
-  {
+  if constexpr (FA2_STORE_LDS && !PP) {
+    // every wave passed the last tile's barrier: the K/V buffers are free for the staging image
+    uint16_t* o0 = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qw0 * p.o_stride[1];
+    store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, inv, row_ok, o0, p.o_stride[1],
+                             min(32, p.seqlen_q - qw0), D, lane);
+  } else {
     uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
     const bool row_in = qi < p.seqlen_q;
 #pragma unroll
