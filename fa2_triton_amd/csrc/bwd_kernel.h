@@ -31,6 +31,9 @@
 
 namespace fa2 {
 
+#ifndef FA2_DKDV_DESC
+#define FA2_DKDV_DESC 1  // dkdv_kernel sweeps query tiles last to first (L2 reuse across key blocks)
+#endif
 #ifndef FA2_DKDV_LS
 #define FA2_DKDV_LS 2
 #endif
@@ -172,6 +175,13 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   int m_begin = 0;
   if (CAUSAL) m_begin = max(0, n0 - diag) & ~(BMQ - 1);
   const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
+  // Query tiles are swept from the last one down (DESC): every workgroup of a (batch, kv-head)
+  // then reads the same Q / dO tile at the same step -- one HBM read, the other key blocks hit
+  // L2 -- where an ascending sweep from each block's own first visible tile spreads the reads
+  // of one tile over the whole pass.  (The dS path keeps the ascending order of its workspace.)
+  constexpr bool DESC = FA2_DKDV_DESC && !DSOUT;
+  const int m_last = m_begin + (n_mt - 1) * BMQ;
+  auto tile_row = [&](int t) { return DESC ? m_last - t * BMQ : m_begin + t * BMQ; };
   const int total = n_mt * G;  // (q-head, tile) steps
 
   // buffer-resource LDS-DMA (rows past Lq read as zeros; masked out of every product)
@@ -186,7 +196,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   int st_g = 0, st_mt = 0;  // (q-head in group, query tile) of the next step to stage
   auto stage = [&](int buf) {
     const int hq = h0 + st_g;
-    const int m = m_begin + st_mt * BMQ;
+    const int m = tile_row(st_mt);
     if (++st_mt == n_mt) {
       st_mt = 0;
       ++st_g;
@@ -494,7 +504,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     const int cur = step & 1;
     if (step + 1 < total) stage(cur ^ 1);
     const int hq = h0 + g;
-    const int m = m_begin + mt * BMQ;
+    const int m = tile_row(mt);
     // wave-uniform tile class
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
     const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);

@@ -65,8 +65,9 @@ def test_ds_path_matches_recompute_path(b, hq, hkv, sq, sk, d, causal, use_mask,
     without = _grads(q, k, v, do, mask, bias, dropout_p, seed, causal, False)
     for a, r, name in zip(with_ds, without, ("dq", "dk", "dv")):
         assert torch.isfinite(a).all(), name
-        if name == "dv":  # P^T dO: the same kernel code either way
-            assert torch.equal(a, r), name
+        if name == "dv":  # P^T dO: the same products, summed over the query tiles in ascending
+            # order on the dS path and descending on the recompute path: within one rounding
+            torch.testing.assert_close(a.float(), r.float(), rtol=1e-2, atol=1e-3 * r.float().abs().max().item())
         else:  # dQ: dS rounding; dK: delta = rowsum(O dO) summed in another order (delta_kernel
             # here, dq_kernel's fused row sum there)
             torch.testing.assert_close(a.float(), r.float(), rtol=2e-2, atol=2e-3 * r.float().abs().max().item())
