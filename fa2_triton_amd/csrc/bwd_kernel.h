@@ -222,6 +222,54 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       else blds4(voff, make_rsrc(p.delta + row0, BMQ * 4), lds);
     }
   };
+  // The same staging for the descending sweep with every address carried from step to step in
+  // SGPRs: the byte address of the next tile's first Q / dO row and the index of its first
+  // LSE2 / delta row move by one tile per step and jump to the next q-head's last tile when the
+  // head changes, so a step's staging is a few scalar adds and the descriptor words.  (Recomputed
+  // per step from the head and row indices, the 64-bit address arithmetic of `stage` put ~130
+  // scalar instructions in front of every step; a timing ablation without it ran 4-7 % faster.)
+  const int64_t q_rb = p.q_stride[1] * 2, o_rb = p.do_stride[1] * 2;  // row bytes
+  uint64_t nq = 0, no = 0;  // next tile's first-row byte addresses
+  int64_t nl = 0;           // next tile's first LSE2 / delta element
+  int nm = m_last;          // next tile's first row
+  if constexpr (DESC && ALIGNED) {
+    nq = uniform64((int64_t)(uintptr_t)p.q + 2 * (b * p.q_stride[0] + h0 * p.q_stride[2]) + (int64_t)m_last * q_rb);
+    no = uniform64((int64_t)(uintptr_t)p.dout + 2 * (b * p.do_stride[0] + h0 * p.do_stride[2]) + (int64_t)m_last * o_rb);
+    nl = uniform64((int64_t)(b * p.heads_q + h0) * p.lse_row_stride + m_last);
+  }
+  const int64_t q_wrap = (int64_t)(n_mt - 1) * BMQ * q_rb + 2 * p.q_stride[2];
+  const int64_t o_wrap = (int64_t)(n_mt - 1) * BMQ * o_rb + 2 * p.do_stride[2];
+  const int64_t l_wrap = (int64_t)(n_mt - 1) * BMQ + p.lse_row_stride;
+  auto stage_desc = [&](int buf) {
+    const int rows = Lq - nm;  // >= 1: rows past Lq read as zeros (descriptor range)
+    const i32x4 rq = make_rsrc((const void*)(uintptr_t)nq, (uint32_t)min(rows, qrows) * (uint32_t)q_rb);
+    const i32x4 ro = make_rsrc((const void*)(uintptr_t)no, (uint32_t)min(rows, orows) * (uint32_t)o_rb);
+#pragma unroll
+    for (int it = 0; it < BufStager<DT, BMQ, NT>::kIters; ++it) {
+      qst.piece(qt(buf), rq, it);
+      ost.piece(ot(buf), ro, it);
+    }
+    if (w == 0) {
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf)));
+      int t = threadIdx.x;
+      asm volatile("" : "+v"(t));
+      const uint32_t voff = (uint32_t)(t & 31) * 4u;
+      if (((t >> 5) & 1) == 0) blds4(voff, make_rsrc(p.lse + nl, BMQ * 4), lds);
+      else blds4(voff, make_rsrc(p.delta + nl, BMQ * 4), lds);
+    }
+    if (++st_mt == n_mt) {
+      st_mt = 0;
+      nm = m_last;
+      nq = uniform64(nq + q_wrap);
+      no = uniform64(no + o_wrap);
+      nl = uniform64(nl + l_wrap);
+    } else {
+      nm -= BMQ;
+      nq = uniform64(nq - BMQ * q_rb);
+      no = uniform64(no - BMQ * o_rb);
+      nl = uniform64(nl - BMQ);
+    }
+  };
 
   u32x4 kf[KS];
   {
@@ -232,7 +280,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   if (total > 0) {
     const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
     stage_tile<DT, BNK, NT, ALIGNED>(Vs, vg, p.v_stride[1], n0, Lk, D, tid);
-    stage(0);
+    if constexpr (DESC && ALIGNED) stage_desc(0);
+    else stage(0);
   }
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
@@ -502,7 +551,10 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   int g = 0, mt = 0;  // (q-head in group, query tile) of the current step
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
-    if (step + 1 < total) stage(cur ^ 1);
+    if (step + 1 < total) {
+      if constexpr (DESC && ALIGNED) stage_desc(cur ^ 1);
+      else stage(cur ^ 1);
+    }
     const int hq = h0 + g;
     const int m = tile_row(mt);
     // wave-uniform tile class

@@ -365,7 +365,12 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
     float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
     lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
   }
-  if (qi < p.seqlen_q) {
+  if constexpr (FA2_STORE_LDS && ALIGNED) {
+    // every loop iteration ends in a barrier: the K/V buffers (NW x 32 rows x DT fit exactly) are free
+    uint16_t* o0 = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qw0 * p.o_stride[1];
+    store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, inv, row_ok, o0, p.o_stride[1],
+                             min(32, p.seqlen_q - qw0), D, lane);
+  } else if (qi < p.seqlen_q) {
     uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
