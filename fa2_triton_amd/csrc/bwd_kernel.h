@@ -909,7 +909,8 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   // Interior tiles (no mask, no bias, no dropout): the two 32-key halves are software
   // pipelined inside the tile so that every softmax-gradient VALU op sits beside an MFMA of
   // the same wave:
-  //   [S, dP of half 0] [S, dP of half 1 | dS of half 0] [dQ of half 0 | dS of half 1] [dQ of half 1]
+  //   [S, dP of half 0] [S, dP of half 1 | dS of half 0] [dQ of half 0 | dS 0-7 of half 1]
+  //   [dQ of half 1 | dS 8-15 of half 1 beside its first steps]
   auto tile_pipe = [&](const char* K, const char* V) {
     constexpr int L = kDqPipeLead;  // two score pairs live: one step of fragments in flight
     f32x16 s[2], dp[2];
@@ -963,11 +964,21 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 #pragma unroll
       for (int e = st * 16 / SDP_STEPS; e < (st + 1) * 16 / SDP_STEPS; ++e) ds_elem(0, e);
     });
-    dq_half(0, [&](int st) {  // 16 dS elements of half 1 over the dQ steps of half 0
+    // dS of half 1: elements 0-7 (packed fragment dsp[1][0]) beside the dQ steps of half 0,
+    // elements 8-15 (dsp[1][1], first read at step DQ_STEPS / 2 of dq_half(1)) beside the dQ
+    // steps of half 1 that read dsp[1][0].  (All 16 over half 0's dQ steps: 1.8 % slower causal,
+    // profiles/r02_ab_dq_spread.txt.)
+    dq_half(0, [&](int st) {
 #pragma unroll
-      for (int e = st * 16 / DQ_STEPS; e < (st + 1) * 16 / DQ_STEPS; ++e) ds_elem(1, e);
+      for (int e = st * 8 / DQ_STEPS; e < (st + 1) * 8 / DQ_STEPS; ++e) ds_elem(1, e);
     });
-    dq_half(1, [](int) {});
+    dq_half(1, [&](int st) {
+      constexpr int H = DQ_STEPS / 2;
+      if (st < H) {
+#pragma unroll
+        for (int e = 8 + st * 8 / H; e < 8 + (st + 1) * 8 / H; ++e) ds_elem(1, e);
+      }
+    });
   };
 
   for (int it = 0; it < ntiles; ++it) {
