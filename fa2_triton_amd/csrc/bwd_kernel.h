@@ -46,6 +46,9 @@ namespace fa2 {
 constexpr int kDkdvLS = FA2_DKDV_LS;
 constexpr int kDkdvLD = FA2_DKDV_LD;
 constexpr int kDkdvLT = FA2_DKDV_LT;
+#ifndef FA2_DQ_PAIR
+#define FA2_DQ_PAIR 1  // dq_kernel: mirrored pairs of row blocks per workgroup (0 never, 1 causal, 2 always)
+#endif
 #ifndef FA2_DQ_LEAD
 #define FA2_DQ_LEAD 2
 #endif
@@ -733,11 +736,18 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
+  // work items head-major per XCD (xcd_item), heaviest first; with FA2_DQ_PAIR a workgroup runs
+  // a mirrored pair of row blocks of one head (nmb-1-j, then j: equal causal work per workgroup)
   const int nmb = (p.seqlen_q + BM - 1) / BM;
-  const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
-  const int bh = item / nmb;
-  const int mbi = item - bh * nmb;
-  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;  // heaviest blocks first
+  constexpr bool PAIR = FA2_DQ_PAIR >= 2 || (FA2_DQ_PAIR == 1 && CAUSAL);
+  const int per_bh = PAIR ? (nmb + 1) / 2 : nmb;
+  const int item = xcd_item(blockIdx.x, gridDim.x);
+  const int bh = item / per_bh;
+  const int mbi = item - bh * per_bh;
+  const int nrep = PAIR && nmb - 1 - mbi != mbi ? 2 : 1;
+  for (int rep = 0; rep < nrep; ++rep) {
+  if (rep > 0) __syncthreads();  // every wave is past the first item's LDS epilogue
+  const int mb = PAIR ? (rep == 0 ? nmb - 1 - mbi : mbi) : (CAUSAL ? (nmb - 1 - mbi) : mbi);
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
   int Lq = p.seqlen_q, Lk = p.seqlen_k;
@@ -1037,6 +1047,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
       }
     }
   }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1274,7 +1285,9 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   }
   if ((stages & 4) && a.seqlen_q > 0) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
-    dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+    constexpr bool PAIR = FA2_DQ_PAIR >= 2 || (FA2_DQ_PAIR == 1 && CAUSAL);
+    const int nmb = (a.seqlen_q + BM - 1) / BM;
+    dim3 grid((PAIR ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
     else

@@ -24,6 +24,10 @@
 
 namespace fa2 {
 
+#ifndef FA2_FWD_PAIR
+#define FA2_FWD_PAIR 1  // mirrored pairs of row blocks per workgroup: 0 never, 1 causal only, 2 always
+#endif
+
 #ifndef FA2_FWD_PP
 #define FA2_FWD_PP 0  // ping-pong schedule: 0 never, 1 non-causal only, 2 always
 #endif
@@ -55,12 +59,20 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int r32 = lane & 31, hh = lane >> 5;
 
-  // ---- work item (as fwd_kernel: head-major per XCD, heaviest first) -----------------------
+  // ---- work items -------------------------------------------------------------------------
+  // Head-major per XCD (xcd_item), heaviest first.  With FA2_FWD_PAIR each workgroup runs a
+  // mirrored pair of row blocks of one head, nmb-1-j then j (equal causal work per workgroup,
+  // half the workgroup launches; the second item starts after a barrier).
   const int nmb = (p.seqlen_q + BM - 1) / BM;
+  constexpr bool PAIR = FA2_FWD_PAIR >= 2 || (FA2_FWD_PAIR == 1 && CAUSAL);
+  const int per_bh = PAIR ? (nmb + 1) / 2 : nmb;
   const int item = xcd_item(blockIdx.x, gridDim.x);
-  const int bh = item / nmb;
-  const int mbi = item - bh * nmb;
-  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;
+  const int bh = item / per_bh;
+  const int mbi = item - bh * per_bh;
+  const int nrep = PAIR && nmb - 1 - mbi != mbi ? 2 : 1;
+  for (int rep = 0; rep < nrep; ++rep) {
+  if (rep > 0) __syncthreads();  // every wave is past the first item's LDS epilogue
+  const int mb = PAIR ? (rep == 0 ? nmb - 1 - mbi : mbi) : (CAUSAL ? (nmb - 1 - mbi) : mbi);
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
   int Lq = p.seqlen_q, Lk = p.seqlen_k;
@@ -449,12 +461,15 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
       }
     }
   }
+  }
 }
 
 template <bool BF16, int DT, bool CAUSAL, bool PP>
 static hipError_t launch_fwd_pipe_t(const fa2_fwd_args& a, hipStream_t st) {
   constexpr int NW = PipeCfg<PP>::NW, BM = NW * 32;
-  dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
+  constexpr bool PAIR = FA2_FWD_PAIR >= 2 || (FA2_FWD_PAIR == 1 && CAUSAL);
+  const int nmb = (a.seqlen_q + BM - 1) / BM;
+  dim3 grid((PAIR ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
   hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, PP>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
