@@ -94,8 +94,6 @@ class BwdArgs(ctypes.Structure):
         ("softmax_scale", ctypes.c_float),
         ("dropout_p", ctypes.c_float),
         ("dropout_seed", ctypes.c_uint64),
-        ("ds_workspace", ctypes.c_void_p),
-        ("ds_workspace_bytes", ctypes.c_int64),
         ("dbias", ctypes.c_void_p),
         ("dbias_stride", _i64x3),
         ("dkv_workspace", ctypes.c_void_p),
@@ -103,9 +101,9 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 4  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 5  # FA2_ABI_VERSION in include/fa2_amd.h
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_ds_workspace_bytes", "fa2_bwd_dkv_workspace_bytes",
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes",
                     "fa2_cu_seqlens_from_mask",
                     "fa2_last_error", "fa2_version")
 
@@ -133,8 +131,6 @@ def load() -> ctypes.CDLL:
         lib.fa2_bwd.restype = ctypes.c_int
         lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.c_void_p]
         lib.fa2_bwd_stages.restype = ctypes.c_int
-        lib.fa2_bwd_ds_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
-        lib.fa2_bwd_ds_workspace_bytes.restype = ctypes.c_int64
         lib.fa2_bwd_dkv_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
         lib.fa2_bwd_dkv_workspace_bytes.restype = ctypes.c_int64
         lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,

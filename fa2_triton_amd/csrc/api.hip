@@ -113,8 +113,9 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   if (a->dq_dtype != a->dtype && a->dq_dtype != FA2_F32) return fail(FA2_E_INVALID, "dq dtype %d", a->dq_dtype);
   if (a->bias && a->bias_dtype != FA2_F16 && a->bias_dtype != FA2_BF16 && a->bias_dtype != FA2_F32)
     return fail(FA2_E_INVALID, "bias dtype %d", a->bias_dtype);
-  if (stages & ~7) return fail(FA2_E_INVALID, "stage mask %d", stages);
+  if (stages & ~15) return fail(FA2_E_INVALID, "stage mask %d", stages);
   if (a->dbias && !a->bias) return fail(FA2_E_INVALID, "dbias requested without a bias");
+  if ((stages & 8) && !a->dbias) return fail(FA2_E_INVALID, "stage 8 (bias gradient) without a dbias buffer");
   if (a->seqlen_q == 0 && a->seqlen_k == 0) return FA2_OK;  // empty dQ, dK, dV
   const int D = a->head_dim;
   bool aligned = vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
@@ -125,14 +126,6 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
     aligned = aligned && aligned16(a->dq) && a->dq_stride[0] % 4 == 0 && a->dq_stride[1] % 4 == 0 && a->dq_stride[2] % 4 == 0;
   else
     aligned = aligned && vec_ok(D, a->dq, a->dq_stride);
-  if (a->ds_workspace) {
-    const int64_t need = fa2_bwd_ds_workspace_bytes(a);
-    if (need == 0)
-      return fail(FA2_E_INVALID, "ds_workspace given but the dS path does not apply (head_dim %d, or unaligned tensors)", D);
-    if (a->ds_workspace_bytes < need)
-      return fail(FA2_E_INVALID, "ds_workspace_bytes %lld < %lld required", (long long)a->ds_workspace_bytes, (long long)need);
-    if (!aligned16(a->ds_workspace)) return fail(FA2_E_INVALID, "ds_workspace must be 16-byte aligned");
-  }
   if (a->dkv_workspace) {
     const int64_t need = fa2_bwd_dkv_workspace_bytes(a);
     if (need == 0) return fail(FA2_E_INVALID, "dkv_workspace given but no dK/dV split applies to these sizes");
@@ -157,23 +150,7 @@ int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
   return hip_status(e, "fa2_bwd launch");
 }
 
-int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, a && a->ds_workspace ? 7 : 6, stream); }
-
-int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* a) {
-  // head dims 72..128 (multiples of 8): at D <= 64 recomputing S and dP costs less than the dS
-  // stream (measured at B=8 H=16 S=1024 D=64: fwd+bwd 0.30 ms recompute, 0.34 ms dS); the
-  // dq_ds_kernel ring of D = 256 tiles would not fit in LDS.  The path also needs the 16-byte
-  // vector layout of every tensor it reads (the aligned kernels), so the pointers and strides
-  // of Q, K, V, O and dO must be filled in before this call.
-  if (!a || a->head_dim % 8 != 0 || a->head_dim <= 64 || a->head_dim > 128 || a->batch < 1 || a->heads_q < 1) return 0;
-  if (a->seqlen_q <= 0 || a->seqlen_k <= 0) return 0;
-  const int D = a->head_dim;
-  if (!(vec_ok(D, a->q, a->q_stride) && vec_ok(D, a->k, a->k_stride) && vec_ok(D, a->v, a->v_stride) &&
-        vec_ok(D, a->o, a->o_stride) && vec_ok(D, a->dout, a->do_stride) && a->k_stride[1] == a->v_stride[1]))
-    return 0;
-  const fa2::DsLayout L(a->seqlen_q, a->seqlen_k, a->causal != 0);
-  return (int64_t)a->batch * a->heads_q * L.per_head() * (32 * 32 * 2);
-}
+int fa2_bwd(const fa2_bwd_args* a, void* stream) { return fa2_bwd_stages(a, a && a->dbias ? 14 : 6, stream); }
 
 int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* a) {
   if (!a || a->seqlen_q <= 0 || a->seqlen_k <= 0 || a->head_dim < 1) return 0;

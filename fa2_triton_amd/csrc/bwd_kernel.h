@@ -1,4 +1,4 @@
-// bwd.hip -- FlashAttention-2 backward for gfx950 (CDNA4).
+// bwd_kernel.h -- FlashAttention-2 backward for gfx950 (CDNA4).
 //
 // Replaces the reference's backward launches (/root/reference/src/backward/caller.py:95-165):
 //   delta_kernel  <- _compute_delta        (/root/reference/src/backward/compute_delta.py:17-73);
@@ -19,65 +19,20 @@
 #include "common.h"
 #include "fa2_internal.h"
 
-// Schedule constants (measured; the variants they replaced are recorded in DESIGN.md §5):
+// Schedule constants (measured; the variants they replaced are recorded in DESIGN.md):
 //  dK/dV: S chain with its Q fragments kDkdvLS MFMAs ahead, then the dP chain with its
-//         (dO, V) fragment pairs kDkdvLD ahead, then the dV/dK steps two transposed fragments
-//         ahead -- at the 256-register limit a deeper prefetch spills;
+//         (dO, V) fragment pairs kDkdvLD ahead, then the dV/dK steps kDkdvLT transposed
+//         fragments ahead -- at the 256-register limit a deeper prefetch spills;
 //  dQ (recompute): fragments kDqLead k-steps ahead; interior tiles software-pipelined by
-//         32-key halves with one step of fragments in flight.
-// The dS workspace is written with non-temporal stores (1.5 % faster dK/dV than plain stores;
-// sc1 / sc0 sc1 / sc1 nt: +38 %, +38 %, +75 %) and read with nt LDS-DMA (a once-read stream).
-#define FA2_DS_LD_POLICY "nt "
+//         32-key halves with kDqPipeLead step of fragments in flight.
 
 namespace fa2 {
 
-#ifndef FA2_DKDV_DESC
-#define FA2_DKDV_DESC 1  // dkdv_kernel sweeps query tiles last to first (L2 reuse across key blocks)
-#endif
-#ifndef FA2_DKDV_LS
-#define FA2_DKDV_LS 2
-#endif
-#ifndef FA2_DKDV_LD
-#define FA2_DKDV_LD 1
-#endif
-#ifndef FA2_DKDV_LT
-#define FA2_DKDV_LT 2
-#endif
-constexpr int kDkdvLS = FA2_DKDV_LS;
-constexpr int kDkdvLD = FA2_DKDV_LD;
-constexpr int kDkdvLT = FA2_DKDV_LT;
-#ifndef FA2_DQ_PAIR
-#define FA2_DQ_PAIR 1  // dq_kernel: mirrored pairs of row blocks per workgroup (0 never, 1 causal, 2 always)
-#endif
-#ifndef FA2_DQ_LEAD
-#define FA2_DQ_LEAD 2
-#endif
-#ifndef FA2_DQ_PIPE_LEAD
-#define FA2_DQ_PIPE_LEAD 1
-#endif
-constexpr int kDqLead = FA2_DQ_LEAD;
-constexpr int kDqPipeLead = FA2_DQ_PIPE_LEAD;
-
-constexpr int kDsChunk = 32 * 32 * 2;  // bytes of one 32-key x 32-query dS tile in the workspace
-constexpr int kDqDsWaves = 8;          // dq_ds_kernel: waves (32 query rows each) per workgroup
-#ifndef FA2_DQDS_BN
-#define FA2_DQDS_BN 32
-#endif
-#ifndef FA2_DQDS_STAGES
-#define FA2_DQDS_STAGES 4
-#endif
-#ifndef FA2_DQDS_QT
-#define FA2_DQDS_QT 2  // non-causal: 2 query tiles per wave (halves the K re-reads; -7 % measured)
-#endif
-#ifndef FA2_DQDS_QT_CAUSAL
-#define FA2_DQDS_QT_CAUSAL 1  // causal: 1 (512-row workgroups balance worse: +4 % measured with 2)
-#endif
-constexpr int kDqDsBN = FA2_DQDS_BN;          // dq_ds_kernel: keys per tile
-template <bool CAUSAL>
-struct DqDsQT {  // dq_ds_kernel: 32-query tiles per wave
-  static constexpr int value = CAUSAL ? FA2_DQDS_QT_CAUSAL : FA2_DQDS_QT;
-};
-constexpr int kDqDsStages = FA2_DQDS_STAGES;  // dq_ds_kernel: ring of K + dS tiles in LDS
+constexpr int kDkdvLS = 2;
+constexpr int kDkdvLD = 1;
+constexpr int kDkdvLT = 2;
+constexpr int kDqLead = 2;
+constexpr int kDqPipeLead = 1;
 
 // ---------------------------------------------------------------------------------------------
 // delta[b, h, i] = -sum_d O[b, i, h, d] * dO[b, i, h, d]   (fp32; 0 for padded rows).  The
@@ -130,7 +85,7 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 // the group's q-heads are dealt to nsplit workgroups per key block, each writes its fp32 partial
 // dK/dV sums to p.dkv_workspace ([nsplit][B][Hkv][Sk][D], unscaled) and dkv_reduce_kernel adds
 // them in split order (deterministic).
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED, bool DSOUT>
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p, int nsplit) {
   using E = Elem<BF16>;
   constexpr int NT = 256;
@@ -178,13 +133,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   int m_begin = 0;
   if (CAUSAL) m_begin = max(0, n0 - diag) & ~(BMQ - 1);
   const int n_mt = (n0 < Lk && m_begin < Lq) ? (Lq - m_begin + BMQ - 1) / BMQ : 0;
-  // Query tiles are swept from the last one down (DESC): every workgroup of a (batch, kv-head)
-  // then reads the same Q / dO tile at the same step -- one HBM read, the other key blocks hit
-  // L2 -- where an ascending sweep from each block's own first visible tile spreads the reads
-  // of one tile over the whole pass.  (The dS path keeps the ascending order of its workspace.)
-  constexpr bool DESC = FA2_DKDV_DESC && !DSOUT;
+  // Query tiles are swept from the last one down: every workgroup of a (batch, kv-head) then
+  // reads the same Q / dO tile at the same step -- one HBM read, the other key blocks hit L2 --
+  // where an ascending sweep from each block's own first visible tile spreads the reads of one
+  // tile over the whole pass (dkdv HBM reads halved).
   const int m_last = m_begin + (n_mt - 1) * BMQ;
-  auto tile_row = [&](int t) { return DESC ? m_last - t * BMQ : m_begin + t * BMQ; };
+  auto tile_row = [&](int t) { return m_last - t * BMQ; };
   const int total = n_mt * G;  // (q-head, tile) steps
 
   // buffer-resource LDS-DMA (rows past Lq read as zeros; masked out of every product)
@@ -235,7 +189,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   uint64_t nq = 0, no = 0;  // next tile's first-row byte addresses
   int64_t nl = 0;           // next tile's first LSE2 / delta element
   int nm = m_last;          // next tile's first row
-  if constexpr (DESC && ALIGNED) {
+  if constexpr (ALIGNED) {
     nq = uniform64((int64_t)(uintptr_t)p.q + 2 * (b * p.q_stride[0] + h0 * p.q_stride[2]) + (int64_t)m_last * q_rb);
     no = uniform64((int64_t)(uintptr_t)p.dout + 2 * (b * p.do_stride[0] + h0 * p.do_stride[2]) + (int64_t)m_last * o_rb);
     nl = uniform64((int64_t)(b * p.heads_q + h0) * p.lse_row_stride + m_last);
@@ -283,7 +237,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   if (total > 0) {
     const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
     stage_tile<DT, BNK, NT, ALIGNED>(Vs, vg, p.v_stride[1], n0, Lk, D, tid);
-    if constexpr (DESC && ALIGNED) stage_desc(0);
+    if constexpr (ALIGNED) stage_desc(0);
     else stage(0);
   }
   f32x16 dk[NDT], dv[NDT];
@@ -293,11 +247,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   // Phases (sched_barrier-separated so each phase's LDS fragments stay inside it and the
   // register peak stays under 256): S, dP -> P, dS -> dV, dK.
-  // dS tile of the current step in the workspace (DSOUT): chunk (b, hq, q-tile m / 32, key block
-  // kw0 / 32) of the compact layout (DsLayout), advanced by the visible tiles of each q-tile left
-  const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
-  int64_t ds_head = DSOUT ? (int64_t)(b * p.heads_q + h0) * L.per_head() + L.prefix(m_begin >> 5) + (kw0 >> 5) : 0;
-  int64_t ds_chunk = ds_head;
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
@@ -346,17 +295,6 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       hi = qhi - m - 4 * ((ln >> 5) & 1);
     }
     u32x4 pp[2], dsp[2];
-    auto store_ds = [&]() {
-      // publish the rounded dS tile for dq_ds_kernel: chunk (b, hq, q-tile m/32, key block
-      // kw0/32) = 32 key rows of 64 bytes; row kj holds this lane pair's registers as they are
-      // (bytes 32 hh + 16 sp: dsp[sp] = queries 16 sp + 8 (t >> 2) + 4 hh + (t & 3), t = 0..7),
-      // i.e. the queries in the permuted order dq_ds_kernel undoes when it stores dQ.  (Stores
-      // of 1 KiB contiguous per instruction -- register order -- measured no faster here and
-      // made dq_ds_kernel's gather 10 % slower.)
-      char* dst = (char*)p.ds_workspace + ds_chunk * kDsChunk + r32 * 64 + 32 * hh;
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) __builtin_nontemporal_store(dsp[sp], (u32x4*)(dst + 16 * sp));
-    };
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 l4 = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh));
@@ -388,21 +326,12 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
           pv[j] = pr;
           dsv[j] = pr * (dp[i] + d4[j]);  // softmax_scale is applied to dK once, at the end
         }
-        if constexpr (BIAS) {
-          // bias gradient dL/ds_ij = dS (fp32, before rounding): one element per register
-          if (p.dbias != nullptr) {
-            const int qr = m + o + 4 * hh;
-            if (qr < p.seqlen_q && kj < p.seqlen_k)
-              p.dbias[b * p.dbias_stride[0] + hq * p.dbias_stride[1] + (int64_t)qr * p.dbias_stride[2] + kj] = dsv[j];
-          }
-        }
       }
       pp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(pv[0], pv[1]);
       pp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(pv[2], pv[3]);
       dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
-    if constexpr (DSOUT) store_ds();
     __builtin_amdgcn_sched_barrier(0);
     {
       // steps m: dt = m % NDT (independent chains back to back), r = m / NDT: (sp, dV | dK);
@@ -428,11 +357,10 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   // The plain step (no bias, no dropout), software-pipelined inside the wave so that the
   // softmax-gradient VALU work sits beside MFMAs of the same wave instead of in a VALU-only phase:
-  //   [S chain] [dP chain | P = exp2(S sc - LSE2)] [dV, dK chains | dS = P dP', packs, dS stores]
+  //   [S chain] [dP chain | P = exp2(S sc - LSE2)] [dV, dK chains | dS = P dP', packs]
   // The dP accumulator starts at -delta (the delta workspace holds -rowsum(O dO)), so the chain
   // yields dP - delta and dS is one multiply; the LSE2 and -delta rows are read from LDS at the
-  // start of the step, long before their use.  (The dS-workspace path keeps `body`: with its dS
-  // stores issued inside the dV/dK chain this schedule measured 1-13 % slower there, DESIGN.md.)
+  // start of the step, long before their use.
   auto body_pipe = [&](auto mask_c, const char* Q, const char* O, const char* S, int m) {
     constexpr bool MASK = decltype(mask_c)::value;
     constexpr int LS = kDkdvLS < KS ? kDkdvLS : KS, LD = kDkdvLD < KS ? kDkdvLD : KS;
@@ -555,7 +483,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
     if (step + 1 < total) {
-      if constexpr (DESC && ALIGNED) stage_desc(cur ^ 1);
+      if constexpr (ALIGNED) stage_desc(cur ^ 1);
       else stage(cur ^ 1);
     }
     const int hq = h0 + g;
@@ -564,7 +492,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
     const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);
     if (!dead) {
-      if constexpr (!BIAS && !DROPOUT && !DSOUT) {
+      if constexpr (!BIAS && !DROPOUT) {
         if (need_mask)
           body_pipe(std::true_type{}, qt(cur), ot(cur), st(cur), m);
         else
@@ -576,24 +504,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
           body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
       }
     }
-    if constexpr (DSOUT) {
-      // the 2 dS stores of this step were issued after the next tile's LDS-DMA: wait for all
-      // but them (vmcnt retires in issue order) and use a raw barrier, whose __syncthreads()
-      // form would drain the stores too; they complete under the next step
-      if (__builtin_amdgcn_readfirstlane(dead))
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      vm_wait_all();
-      __syncthreads();
-    }
+    vm_wait_all();
+    __syncthreads();
     if (++mt == n_mt) {
       mt = 0;
       ++g;
-      if constexpr (DSOUT) ds_chunk = ds_head = uniform64(ds_head + L.per_head());
-    } else if constexpr (DSOUT) {
-      ds_chunk = uniform64(ds_chunk + min(max((m >> 5) + L.c, 0), L.nkt));  // nvis of the q-tile left behind
     }
   }
 
@@ -633,7 +548,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
     return;
   }
-  if constexpr (FA2_STORE_LDS && ALIGNED) {
+  if constexpr (ALIGNED) {
     // every wave passed the last step's barrier: V and Q/dO buffers hold the staging images
     uint16_t* k0 = (uint16_t*)p.dk + b * p.dk_stride[0] + hkv * p.dk_stride[2] + (int64_t)kw0 * p.dk_stride[1];
     uint16_t* v0 = (uint16_t*)p.dv + b * p.dv_stride[0] + hkv * p.dv_stride[2] + (int64_t)kw0 * p.dv_stride[1];
@@ -736,10 +651,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
-  // work items head-major per XCD (xcd_item), heaviest first; with FA2_DQ_PAIR a workgroup runs
+  // work items head-major per XCD (xcd_item), heaviest first; under a causal mask a workgroup runs
   // a mirrored pair of row blocks of one head (nmb-1-j, then j: equal causal work per workgroup)
   const int nmb = (p.seqlen_q + BM - 1) / BM;
-  constexpr bool PAIR = FA2_DQ_PAIR >= 2 || (FA2_DQ_PAIR == 1 && CAUSAL);
+  constexpr bool PAIR = CAUSAL;
   const int per_bh = PAIR ? (nmb + 1) / 2 : nmb;
   const int item = xcd_item(blockIdx.x, gridDim.x);
   const int bh = item / per_bh;
@@ -1009,7 +924,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     __syncthreads();
   }
 
-  if constexpr (FA2_STORE_LDS && ALIGNED && !DQF32) {
+  if constexpr (ALIGNED && !DQF32) {
     // the last tile's barrier is behind every wave: the K/V buffers hold the staging images
     uint16_t* q0 = (uint16_t*)p.dq + b * p.dq_stride[0] + hq * p.dq_stride[2] + (int64_t)mw0 * p.dq_stride[1];
     store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, scale, qvalid, q0, p.dq_stride[1],
@@ -1051,193 +966,178 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// dQ from stored dS (the dS-workspace path): dQ = scale * dS K, with dS the rounded tiles that
-// dkdv_kernel<..., DSOUT> published.  The same product as dq_kernel's last GEMM
-// (/root/reference/src/backward/compute_dq.py:70-76), without its recompute of S = Q K^T and
-// dP = dO V^T: the pass streams 2 bytes of dS per (query, key) pair from HBM and runs one GEMM
-// instead of three.  One workgroup = 8 waves = 256 query rows of one (batch, q-head); per 64-key
-// tile the K rows (shared by the 8 waves) and each wave's two dS chunks are LDS-DMA'd into a
-// ring of 3 buffers, two tiles in flight (counted vmcnt, raw barriers).
-//   dQ^T[d][q] += K^T dS^T   A = K^T (ds_read_b64_tr_b16 of the K tile),
-//                            B = dS^T (ds_read_b64_tr_b16 of the [key][q] chunk image)
-// A wave reads the chunk of key block j iff dkdv_kernel wrote it: 32 j < Lk and, causal,
-// 32 j <= (first row of the wave) + 31 + (Lk - Lq) -- the complement of dkdv_kernel's `dead`.
-template <bool BF16, int DT, bool CAUSAL, bool DQF32>
-__global__ void __launch_bounds__(kDqDsWaves * 64, 1) dq_ds_kernel(const fa2_bwd_args p) {
+// Bias gradient (ABI 5; the reference has none, /root/reference/src/wrapper.py:86):
+//   dbias[b', h', i, j] = sum over the (batch, q-head) pairs the bias broadcasts to of
+//                         dS[b, hq, i, j] = P (dP~ - delta),   P = exp2(s scale log2e + bias log2e - LSE2)
+// (dP~ = dP M / (1 - p) under dropout, M the forward's keep mask), in fp32, deterministic: one
+// workgroup owns 128 rows of one bias slice (b', h') and adds the pairs of its broadcast group one
+// after the other into those rows (the first pair stores, the next ones read-add-store their own
+// earlier writes), so the memory is the bias-shaped output alone -- no [B, Hq, Sq, Sk] buffer.
+// The workgroup's keys are a chunk of kDbiasChunk tiles, so that a broadcast bias still spreads
+// over (Sq / 128) x (Sk / 512) workgroups per slice.
+// Per pair the structure is dq_kernel's (query on the lane, Q / dO in registers, 64-key K/V tiles
+// in LDS): S^T = K Q^T and dP^T = V dO^T (the same products as compute_dq.py:38-69), without the
+// dQ GEMM.  delta comes from the dQ (or delta) kernel that ran before (-rowsum(O dO), negated).
+constexpr int kDbiasChunk = 8;  // 64-key tiles per dbias workgroup
+
+template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
+__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = kDqDsWaves, NT = NW * 64;
-  constexpr int QT = DqDsQT<CAUSAL>::value;   // 32-query tiles per wave (each K fragment feeds QT MFMAs)
-  constexpr int BN = kDqDsBN, HB = BN / 32;   // keys per tile
-  constexpr int BM = NW * 32 * QT;
-  constexpr int NDT = DT / 32;
-  constexpr int KTILE = BN * DT * 2;          // K tile bytes
-  constexpr int DSQ = HB * kDsChunk;          // dS image of one query tile: BN keys x 32 queries
-  constexpr int DSW = QT * DSQ;               // one wave's dS images of a tile
-  constexpr int BUF = KTILE + NW * DSW;
-  constexpr int NBUF = kDqDsStages < (160 * 1024) / BUF ? kDqDsStages : (160 * 1024) / BUF;
-  static_assert(NBUF >= 3 && NBUF <= 6, "ring of 3..6 buffers");
-  constexpr int KP = BufStager<DT, BN, NT>::kIters;  // K pieces per lane and tile
-  static_assert(BufStager<DT, BN, NT>::kPieces % NT == 0, "every lane issues the same K pieces");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+  constexpr int NT = 256, BM = 128, BN = 64;
+  constexpr int KS = DT / 16;
+  constexpr int TILE = BN * DT * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = lane >> 5;
-  const int nmb = (p.seqlen_q + BM - 1) / BM;
-  const int item = xcd_item(blockIdx.x, gridDim.x);
-  const int bh = item / nmb;
-  const int mbi = item - bh * nmb;
-  const int mb = CAUSAL ? (nmb - 1 - mbi) : mbi;  // heaviest blocks first
-  const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
-  const int hkv = hq / (p.heads_q / p.heads_kv);
-  int Lq = p.seqlen_q, Lk = p.seqlen_k;
-  if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nkt = (p.seqlen_k + BN - 1) / BN;        // key tiles of the output rows
+  const int nkc = (nkt + kDbiasChunk - 1) / kDbiasChunk;
+  const int mb = blockIdx.x / nkc, kc = blockIdx.x - mb * nkc;
+  const int t0 = kc * kDbiasChunk, t1 = min(nkt, t0 + kDbiasChunk);  // this workgroup's key tiles
+  const int Hb = p.bias_stride[1] != 0 ? p.heads_q : 1;
+  const int slice = blockIdx.y;                       // (b', h') of the bias
+  const int bb = slice / Hb, hb = slice - bb * Hb;
+  const bool sum_b = p.bias_stride[0] == 0, sum_h = p.bias_stride[1] == 0;
+  const int nb = sum_b ? p.batch : 1, nh = sum_h ? p.heads_q : 1;
   const int D = p.head_dim;
-  const int diag = Lk - Lq;
-  const int m0 = mb * BM;
-  const int mw0 = m0 + 32 * QT * w;  // first row of this wave's first query tile
-  // column c = 16 hh + 8 sp + t of a dS chunk row is query 16 sp + 8 (t >> 2) + 4 hh + (t & 3)
-  // of the tile (dkdv_kernel stores its registers as they are): the accumulator column of this
-  // lane is that query
-  const int c = lane & 31;
-  const int qoff = 16 * ((c >> 3) & 1) + 8 * ((c & 7) >> 2) + 4 * (c >> 4) + (c & 3);
+  const int mw0 = mb * BM + 32 * w;
+  const int qi = mw0 + r32;                          // this lane's row
+  const float scale2 = p.softmax_scale * kLog2e;
+  float* drow = p.dbias + bb * p.dbias_stride[0] + hb * p.dbias_stride[1] + (int64_t)(qi < p.seqlen_q ? qi : 0) * p.dbias_stride[2];
+  const bool row_in = qi < p.seqlen_q;
 
-  int n_end = 0;  // keys any row of the workgroup sees
-  if (m0 < Lq) n_end = max(CAUSAL ? min(Lk, m0 + BM + diag) : Lk, 0);
-  // keys any row of query tile j of this wave sees: its chunk kt was written iff 32 kt < nw_end[j]
-  int nw_end[QT];
-#pragma unroll
-  for (int j = 0; j < QT; ++j) {
-    const int mj = mw0 + 32 * j;
-    nw_end[j] = mj < Lq ? max(CAUSAL ? min(Lk, mj + 32 + diag) : Lk, 0) : 0;
-  }
-  int nw_max = 0;  // keys any row of the wave sees (tiles past Lq see none)
-#pragma unroll
-  for (int j = 0; j < QT; ++j) nw_max = max(nw_max, nw_end[j]);
-  const int ntiles = (n_end + BN - 1) / BN;
-
-  const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
-  auto ktile = [&](int buf) { return smem + buf * BUF; };
-  auto dtile = [&](int buf, int j) { return smem + buf * BUF + KTILE + w * DSW + j * DSQ; };
+  auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
+  auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
   BufStager<DT, BN, NT> kst;
-  kst.init(tid, p.k_stride[1], D);
-  const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
-  // chunk row of query tile j: its visible chunks (b, hq, q-tile, 0 .. nvis) are contiguous
-  // (DsLayout, fa2_internal.h); the range ends
-  // at the tile's last written chunk, so the DMA of a chunk past it reads zeros and every lane
-  // issues the same number of pieces per stage (counted vmcnt below)
-  const DsLayout L(p.seqlen_q, p.seqlen_k, CAUSAL);
-  const int nkt = L.nkt;
-  i32x4 drs[QT];
-#pragma unroll
-  for (int j = 0; j < QT; ++j) {
-    const int64_t crow = (int64_t)bh * L.per_head() + L.prefix((mw0 >> 5) + j);
-    drs[j] = make_rsrc((const char*)p.ds_workspace + crow * kDsChunk,
-                       (uint32_t)min(nkt, (nw_end[j] + 31) >> 5) * kDsChunk);
-  }
-  // piece it of this lane: 16 bytes of the image of a query tile's HB chunks; the image is a
-  // Tile<32, BN> ([BN keys][32 query columns], swizzled 16-byte chunks), the source row-major
-  uint32_t doff[2 * HB];
-#pragma unroll
-  for (int it = 0; it < 2 * HB; ++it) {
-    const int pc = it * 64 + lane;
-    const int pr = pc >> 2;                          // key row of the image
-    const int cc = (pc & 3) ^ ((pr >> 2) & 3);       // 16-byte column chunk stored at this position
-    doff[it] = (uint32_t)(pr * 64 + cc * 16);        // chunk (pr >> 5) starts at 32 * 64 bytes
-  }
-  auto stage = [&](int buf, int n) {  // KP + 2 HB QT VMEM ops per lane
-    kst.issue(ktile(buf), kg, p.k_stride[1], n, Lk, mrows);
-    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(n >> 5) * kDsChunk);
-#pragma unroll
-    for (int j = 0; j < QT; ++j) {
-      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(dtile(buf, j)));
-#pragma unroll
-      for (int it = 0; it < 2 * HB; ++it) {
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen " FA2_DS_LD_POLICY "lds\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(doff[it]), "s"(drs[j]), "s"(lds + it * 1024), "s"(soff)
-            : "memory");
-      }
-    }
-  };
-  constexpr int VM = KP + 2 * HB * QT;  // VMEM ops per lane and stage
-  // wait until at most `pending` stages (the youngest) are in flight, then a raw barrier:
-  // __syncthreads() would drain the tiles in flight
-  auto wait_keep = [&](int pending) {
-    if (pending >= 4 && NBUF >= 6) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(4 * VM) : "memory");
-    else if (pending >= 3 && NBUF >= 5) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(3 * VM) : "memory");
-    else if (pending >= 2 && NBUF >= 4) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(2 * VM) : "memory");
-    else if (pending >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(VM) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  static_assert(4 * VM < 64, "vmcnt range");
-#pragma unroll
-  for (int j = 0; j < NBUF - 1; ++j)
-    if (j < ntiles) stage(j, j * BN);
-
-  f32x16 acc[QT][NDT];
-#pragma unroll
-  for (int j = 0; j < QT; ++j)
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) acc[j][dt] = zero16();
-  wait_keep(min(NBUF - 2, ntiles - 1));  // tile 0 landed
-
-  int cur = 0;
-  for (int it = 0; it < ntiles; ++it) {
-    const int n0 = it * BN;
-    // tile it + NBUF - 1 goes into the buffer tile it - 1 used (every wave is past its last read)
-    const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
-    if (it + NBUF - 1 < ntiles) stage(nxt, n0 + (NBUF - 1) * BN);
-    const char* K = ktile(cur);
-#pragma unroll
-    for (int t = 0; t < HB; ++t) {
-      // wave-uniform: no query tile of the wave has this chunk
-      if (n0 + 32 * t >= nw_max) break;
-      constexpr int N = 2 * NDT;
-      u32x4 fa[N];
-#pragma unroll
-      for (int m = 0; m < N; ++m) fa[m] = lds_tr_frag<DT, BN>(K, 32 * t + 16 * (m / NDT), 32 * (m % NDT), lane);
-#pragma unroll
-      for (int j = 0; j < QT; ++j) {
-        if (n0 + 32 * t >= nw_end[j]) continue;  // wave-uniform: chunk of tile j not written
-        const char* T = dtile(cur, j);
-        u32x4 fb[2];
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp) fb[sp] = lds_tr_frag<32, BN>(T, 32 * t + 16 * sp, 0, lane);
-#pragma unroll
-        for (int m = 0; m < N; ++m) acc[j][m % NDT] = E::mfma(fa[m], fb[m / NDT], acc[j][m % NDT]);
-      }
-    }
-    // tile it + 1 must have landed; the stages issued after it may stay in flight
-    wait_keep(min(NBUF - 2, ntiles - it - 2));
-    cur = cur == NBUF - 1 ? 0 : cur + 1;
+  int mrows = 0;
+  if (ALIGNED) {
+    kst.init(tid, p.k_stride[1], D);
+    mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
   }
 
-  const float scale = p.softmax_scale;
+  // sixteen dS values of this lane for keys n0 + 32 t + 8 g + 4 hh + (0..3), g = 0..3, into the
+  // output row: the first pair stores, later pairs add to what this lane stored before
+  // (16-byte accesses when the rows allow them: the 4 keys of a group are contiguous)
+  const bool vec4 = ((uintptr_t)p.dbias & 15) == 0 && p.dbias_stride[0] % 4 == 0 && p.dbias_stride[1] % 4 == 0 &&
+                    p.dbias_stride[2] % 4 == 0;
+  auto emit = [&](const f32x16& ds, int n0, int t, bool first) {
+    if (!row_in) return;
 #pragma unroll
-  for (int j = 0; j < QT; ++j) {
-    const int qi = mw0 + 32 * j + qoff;
-    if (qi >= p.seqlen_q) continue;
-    const bool ok = qi < Lq;
-    char* row = (char*)p.dq + (int64_t)(DQF32 ? 4 : 2) * (b * p.dq_stride[0] + hq * p.dq_stride[2] + (int64_t)qi * p.dq_stride[1]);
+    for (int g = 0; g < 4; ++g) {
+      const int k0 = n0 + 32 * t + 8 * g + 4 * hh;
+      if (vec4 && k0 + 4 <= p.seqlen_k) {
+        f32x4 v = {ds[4 * g], ds[4 * g + 1], ds[4 * g + 2], ds[4 * g + 3]};
+        if (!first) v += *(const f32x4*)(drow + k0);
+        *(f32x4*)(drow + k0) = v;
+      } else {
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
-        float a[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = ok ? acc[j][dt][4 * g4 + i] * scale : 0.f;
-        if (d0 < D) {
-          if (DQF32)
-            *(f32x4*)((float*)row + d0) = f32x4{a[0], a[1], a[2], a[3]};
-          else
-            *(u32x2*)((uint16_t*)row + d0) = u32x2{E::pack2(a[0], a[1]), E::pack2(a[2], a[3])};
+        for (int j = 0; j < 4; ++j) {
+          if (k0 + j < p.seqlen_k) {
+            const float v = ds[4 * g + j];
+            drow[k0 + j] = first ? v : drow[k0 + j] + v;
+          }
         }
       }
     }
+  };
+
+  for (int pair = 0; pair < nb * nh; ++pair) {
+    const int b = sum_b ? pair / nh : bb;
+    const int hq = sum_h ? (sum_b ? pair - (pair / nh) * nh : pair) : hb;
+    const bool first = pair == 0;
+    const int hkv = hq / (p.heads_q / p.heads_kv);
+    int Lq = p.seqlen_q, Lk = p.seqlen_k;
+    if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
+    const int diag = Lk - Lq;
+    const int m0 = mb * BM;
+    int n_end = 0;
+    if (m0 < Lq) n_end = max(CAUSAL ? min(Lk, m0 + BM + diag) : Lk, 0);
+    const int tend = min(t1, (n_end + BN - 1) / BN);  // tiles [t0, tend) hold visible pairs
+    const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
+    const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
+    auto stage_kv = [&](int buf, int n) {
+      if constexpr (ALIGNED) {
+        kst.issue(kt(buf), kg, p.k_stride[1], n, Lk, mrows);
+        kst.issue(vt(buf), vg, p.v_stride[1], n, Lk, mrows);
+      } else {
+        stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, Lk, D, tid);
+        stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, Lk, D, tid);
+      }
+    };
+    if (tend > t0) stage_kv(0, t0 * BN);
+    const bool qvalid = qi < Lq;
+    u32x4 qf[KS], of[KS];
+    {
+      const uint16_t* qrow = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2] + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
+      const uint16_t* orow = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2] + (int64_t)(qvalid ? qi : 0) * p.do_stride[1];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        qf[ks] = load_row_frag<ALIGNED>(qrow, 16 * ks + 8 * hh, D, qvalid);
+        of[ks] = load_row_frag<ALIGNED>(orow, 16 * ks + 8 * hh, D, qvalid);
+      }
+    }
+    const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride;
+    const float nlse = qvalid ? -p.lse[srow + qi] : 0.f;
+    const float ndel = qvalid ? p.delta[srow + qi] : 0.f;  // the workspace holds -delta
+    const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + diag + 1) : Lk);
+    uint64_t drop_row = 0;
+    float inv_keep = 1.f;
+    if (DROPOUT) {
+      const uint64_t cu0 = p.cu_seqlens ? (uint64_t)p.cu_seqlens[b] : 0;
+      drop_row = (uint64_t)Lk * (cu0 + (uint64_t)Lq * ((uint64_t)hq + (uint64_t)p.heads_q * (p.cu_seqlens ? 0 : b))) +
+                 (uint64_t)qi * (uint64_t)Lk;
+      inv_keep = 1.f / (1.f - p.dropout_p);
+    }
+    const void* biasb = p.bias;
+    const int64_t bias_row = b * p.bias_stride[0] + hq * p.bias_stride[1] + (int64_t)(qvalid ? qi : 0) * p.bias_stride[2];
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+
+    for (int it = t0; it < tend; ++it) {
+      const int cur = (it - t0) & 1;
+      const int n0 = it * BN;
+      if (it + 1 < tend) stage_kv(cur ^ 1, n0 + BN);
+      const char* K = kt(cur);
+      const char* V = vt(cur);
+      const int rel = lim_lane - n0 - 4 * hh;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
+          dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
+        }
+        f32x16 ds;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int o = 32 * t + (i & 3) + 8 * (i >> 2);
+          const int kj = n0 + o + 4 * hh;
+          const int kc = kj < Lk ? kj : Lk - 1;
+          const float x = fmaf(s[i], scale2, kLog2e * load_bias(biasb, bias_row + kc, p.bias_dtype));
+          float pr = __builtin_amdgcn_exp2f(x + nlse);
+          pr = o < rel ? pr : 0.f;
+          float dpv = dp[i];
+          if (DROPOUT) {
+            const bool keep = philox_uniform(p.dropout_seed, drop_row + (uint64_t)kj) > p.dropout_p;
+            dpv *= keep ? inv_keep : 0.f;
+          }
+          ds[i] = pr * (dpv + ndel);
+        }
+        emit(ds, n0, t, first);
+      }
+      vm_wait_all();
+      __syncthreads();
+    }
+    if (first) {  // key tiles this pair does not see: zeros, so that later pairs can add
+      const f32x16 z = zero16();
+      for (int it = max(tend, t0); it < t1; ++it) {
+        emit(z, it * BN, 0, true);
+        emit(z, it * BN, 1, true);
+      }
+    }
+    vm_wait_all();
   }
 }
 
@@ -1251,30 +1151,6 @@ static void launch_dkv_reduce(const fa2_bwd_args& a, int nsplit, hipStream_t st)
 
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st) {
-  if constexpr (ALIGNED && DT == 128) {  // head dims 72..128 (fa2_bwd_ds_workspace_bytes)
-    if (a.ds_workspace) {
-      // dS path: delta (bit 0), dK/dV + dS tiles (bit 1), dQ = dS K (bit 2)
-      if ((stages & 1) && a.lse_row_stride > 0) {
-        dim3 grid((a.lse_row_stride + 15) / 16, a.batch * a.heads_q);
-        hipLaunchKernelGGL((delta_kernel<BF16, true>), grid, dim3(256), 0, st, a);
-      }
-      if ((stages & 2) && a.seqlen_k > 0) {
-        const int ns = dkv_split(a);
-        dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
-        hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, true, true>), grid, dim3(256), 0, st, a, ns);
-        launch_dkv_reduce<BF16>(a, ns, st);
-      }
-      if ((stages & 4) && a.seqlen_q > 0) {
-        constexpr int BM = kDqDsWaves * 32 * DqDsQT<CAUSAL>::value;
-        dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
-        if (a.dq_dtype == FA2_F32)
-          hipLaunchKernelGGL((dq_ds_kernel<BF16, DT, CAUSAL, true>), grid, dim3(kDqDsWaves * 64), 0, st, a);
-        else
-          hipLaunchKernelGGL((dq_ds_kernel<BF16, DT, CAUSAL, false>), grid, dim3(kDqDsWaves * 64), 0, st, a);
-      }
-      return hipGetLastError();
-    }
-  }
   // order: standalone delta (bit 0), dQ (bit 2; also writes delta), then dK/dV (bit 1, reads it)
   // zero-sized problems launch nothing for that side: Sk == 0 -> dQ = 0 (dq_kernel sees no key
   // tile and writes zeros), no dK/dV rows; Sq == 0 -> dK/dV = 0 (dkdv_kernel sees no query
@@ -1285,7 +1161,7 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   }
   if ((stages & 4) && a.seqlen_q > 0) {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
-    constexpr bool PAIR = FA2_DQ_PAIR >= 2 || (FA2_DQ_PAIR == 1 && CAUSAL);
+    constexpr bool PAIR = CAUSAL;
     const int nmb = (a.seqlen_q + BM - 1) / BM;
     dim3 grid((PAIR ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
     if (a.dq_dtype == FA2_F32)
@@ -1293,10 +1169,16 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     else
       hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
   }
+  if ((stages & 8) && BIAS && a.dbias && a.seqlen_q > 0 && a.seqlen_k > 0) {
+    const int bb = a.bias_stride[0] != 0 ? a.batch : 1, hb = a.bias_stride[1] != 0 ? a.heads_q : 1;
+    const int nkc = ((a.seqlen_k + 63) / 64 + kDbiasChunk - 1) / kDbiasChunk;
+    dim3 grid(((a.seqlen_q + 127) / 128) * nkc, bb * hb);
+    hipLaunchKernelGGL((dbias_kernel<BF16, DT, CAUSAL, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
+  }
   if ((stages & 2) && a.seqlen_k > 0) {
     const int ns = dkv_split(a);
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(256), 0, st, a, ns);
+    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a, ns);
     launch_dkv_reduce<BF16>(a, ns, st);
   }
   return hipGetLastError();

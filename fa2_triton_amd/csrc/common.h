@@ -39,12 +39,6 @@ constexpr float kNegInf = -__builtin_inff();
 // accumulation and bf16/fp16 P (same relative precision at any magnitude) absorb exactly.
 constexpr float kDeferMax = 8.f;
 
-// Epilogue stores of the aligned bf16/fp16 outputs (O, dQ, dK, dV) through LDS, whole rows per
-// store instruction (store_rows_lds); 0 = row-per-lane stores straight from registers.
-#ifndef FA2_STORE_LDS
-#define FA2_STORE_LDS 1
-#endif
-
 // ---------------------------------------------------------------------------------------------
 // Element traits: raw 16-bit storage, conversions and the matching MFMA.
 template <bool BF16>
@@ -443,6 +437,9 @@ FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool vali
   constexpr int NDT = DT / 32;
   constexpr int CPR = DT / 8;   // 16-byte chunks per row
   constexpr int RPI = 64 / CPR;  // rows per store instruction
+  // the row offsets below depend on the lane only: computed from an opaque copy of it, so that
+  // they cannot be hoisted out of a kernel's work-item loop and kept live (spilled) across it
+  asm volatile("" : "+v"(lane));
   const int r = lane & 31, h = lane >> 5;
   const float m = valid ? mul : 0.f;
   char* row = stage + r * (DT * 2);

@@ -18,34 +18,6 @@ hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStr
 hipError_t launch_cu_seqlens(const uint8_t* mask, int64_t stride, int batch, int seqlen,
                              int32_t* out, hipStream_t st);
 
-// dS workspace layout (ABI 3).  Per (batch, q-head) only the 32 x 32 (query, key) tiles that
-// hold a visible pair are stored, q-tile major: q-tile t (rows 32 t ..) sees key tiles
-// 0 .. nvis(t) - 1 with nvis(t) = clamp(t + c, 0, nkt), c = floor((31 + Sk - Sq) / 32) + 1
-// (causal, bottom-right aligned: key j visible to row i iff j <= i + Sk - Sq), c = nkt when not
-// causal.  Tile (t, kt) is number prefix(t) + kt of its (batch, q-head); each is 2 KiB.
-// Varlen (Sq == Sk per batch) sees a subset of the same tiles.
-struct DsLayout {
-  int nqt, nkt, c;
-  __host__ __device__ DsLayout(int sq, int sk, bool causal) {
-    nqt = (sq + 31) >> 5;
-    nkt = (sk + 31) >> 5;
-    const int x = 31 + sk - sq;
-    c = causal ? (x >= 0 ? x / 32 : -((-x + 31) / 32)) + 1 : nkt;
-    if (c > nkt) c = nkt;
-  }
-  // visible tiles of q-tiles 0 .. q-1
-  __host__ __device__ int64_t prefix(int q) const {
-    const int t0 = c < 0 ? -c : 0;                   // first q-tile with a visible key tile
-    const int t1 = nkt - c > 0 ? nkt - c : 0;        // first q-tile that sees all nkt
-    const int64_t a = q < t0 ? q : t0, e = q < t1 ? q : t1;
-    int64_t s = 0;
-    if (e > a) s = (e - a) * (int64_t)c + (e * (e - 1) - a * (a - 1)) / 2;
-    if (q > t1) s += (int64_t)(q - t1) * nkt;
-    return s;
-  }
-  __host__ __device__ int64_t per_head() const { return prefix(nqt); }
-};
-
 // q-head split of dK/dV (ABI 4): the smallest divisor s of the GQA group size G = Hq / Hkv with
 // s * B * Hkv * ceil(Sk / 128) >= kDkvTargetGrid workgroups (two per CU), G if none is; 1 when
 // G == 1 or the grid is already that large.

@@ -39,9 +39,7 @@ struct FwdCfg {
 };
 
 
-#ifndef FA2_OLD_LEAD
-#define FA2_OLD_LEAD 3  // fragment reads in flight ahead of their MFMA (0: compiler order)
-#endif
+constexpr int kFwdLead = 3;  // fragment reads in flight ahead of their MFMA
 
 template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAUSAL>::kWavesPerSimd)) fwd_kernel(const fa2_fwd_args p) {
@@ -149,11 +147,10 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
   auto qk_softmax = [&](auto mask_c, const char* K, int n0, auto fill) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s[2];
-#if FA2_OLD_LEAD
     {
-      // fenced steps: each fragment read runs FA2_OLD_LEAD MFMAs ahead, the two key halves'
+      // fenced steps: each fragment read runs kFwdLead MFMAs ahead, the two key halves'
       // chains alternate
-      constexpr int N = 2 * KS, L = FA2_OLD_LEAD;
+      constexpr int N = 2 * KS, L = kFwdLead;
       u32x4 kf[N];
 #pragma unroll
       for (int j = 0; j < L; ++j) kf[j] = lds_row_frag<DT, BN>(K, 32 * (j & 1), r32, j >> 1, hh);
@@ -167,14 +164,6 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#else
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      s[t] = zero16();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[t] = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s[t]);
-    }
-#endif
     // register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh
     const int rel = lim_lane - n0 - 4 * hh;
     float mx = kNegInf;
@@ -239,9 +228,8 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[dt][i] *= alpha;
     }
-#if FA2_OLD_LEAD
     {
-      constexpr int N = 4 * NDT, L = 2 * FA2_OLD_LEAD > N ? N : 2 * FA2_OLD_LEAD;
+      constexpr int N = 4 * NDT, L = 2 * kFwdLead > N ? N : 2 * kFwdLead;
       u32x4 vf[N];
       auto rd = [&](int m) { return lds_tr_frag<DT, BN>(V, 16 * (m / NDT), 32 * (m % NDT), lane); };
 #pragma unroll
@@ -254,15 +242,6 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#else
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp)
-          acc[dt] = E::mfma(lds_tr_frag<DT, BN>(V, 32 * t + 16 * sp, 32 * dt, lane), pf[t][sp], acc[dt]);
-#endif
   };
 
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
@@ -279,7 +258,7 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
     // With SPREAD the next tile's LDS-DMA pieces ride in the QK^T steps (one every other MFMA)
     // instead of a burst at the top of the tile; rows past the end are clamped, so the issue
     // is branch free (the last tile re-reads valid rows into a buffer nobody reads).
-    constexpr bool SPREAD = ALIGNED && FA2_OLD_LEAD && NT == BN * 4;
+    constexpr bool SPREAD = ALIGNED && NT == BN * 4;
     for (int i = 0; i < ntiles; ++i) {
       const int n0 = i * BN;
       const uint16_t* kgt = kg + (int64_t)(n0 + BN) * p.k_stride[1];
@@ -365,7 +344,7 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
     float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
     lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
   }
-  if constexpr (FA2_STORE_LDS && ALIGNED) {
+  if constexpr (ALIGNED) {
     // every loop iteration ends in a barrier: the K/V buffers (NW x 32 rows x DT fit exactly) are free
     uint16_t* o0 = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qw0 * p.o_stride[1];
     store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, inv, row_ok, o0, p.o_stride[1],

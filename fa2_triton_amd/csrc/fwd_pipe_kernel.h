@@ -24,24 +24,10 @@
 
 namespace fa2 {
 
-#ifndef FA2_FWD_PAIR
-#define FA2_FWD_PAIR 1  // mirrored pairs of row blocks per workgroup: 0 never, 1 causal only, 2 always
-#endif
-
-#ifndef FA2_FWD_PP
-#define FA2_FWD_PP 0  // ping-pong schedule: 0 never, 1 non-causal only, 2 always
-#endif
-
-template <bool PP>
-struct PipeCfg {
-  static constexpr int NW = PP ? 8 : 4;   // waves per workgroup
-  static constexpr int NKB = PP ? 3 : 2;  // K tile buffers
-};
-
-template <bool BF16, int DT, bool CAUSAL, bool PP>
-__global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+template <bool BF16, int DT, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = PipeCfg<PP>::NW, NKB = PipeCfg<PP>::NKB;
+  constexpr int NW = 4, NKB = 2;  // waves per workgroup, K tile buffers
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
@@ -55,16 +41,14 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   __shared__ __attribute__((aligned(16))) char smem[(NKB + 2) * TILE];  // K buffers, V0 V1
   static_assert(NQK % 8 == 0 && 32 % NQK == 0, "QK^T steps must carry whole pack pairs");
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
-  const int r32 = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
 
   // ---- work items -------------------------------------------------------------------------
-  // Head-major per XCD (xcd_item), heaviest first.  With FA2_FWD_PAIR each workgroup runs a
+  // Head-major per XCD (xcd_item), heaviest first.  Under a causal mask each workgroup runs a
   // mirrored pair of row blocks of one head, nmb-1-j then j (equal causal work per workgroup,
   // half the workgroup launches; the second item starts after a barrier).
   const int nmb = (p.seqlen_q + BM - 1) / BM;
-  constexpr bool PAIR = FA2_FWD_PAIR >= 2 || (FA2_FWD_PAIR == 1 && CAUSAL);
+  constexpr bool PAIR = CAUSAL;
   const int per_bh = PAIR ? (nmb + 1) / 2 : nmb;
   const int item = xcd_item(blockIdx.x, gridDim.x);
   const int bh = item / per_bh;
@@ -72,6 +56,7 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   const int nrep = PAIR && nmb - 1 - mbi != mbi ? 2 : 1;
   for (int rep = 0; rep < nrep; ++rep) {
   if (rep > 0) __syncthreads();  // every wave is past the first item's LDS epilogue
+  const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
   const int mb = PAIR ? (rep == 0 ? nmb - 1 - mbi : mbi) : (CAUSAL ? (nmb - 1 - mbi) : mbi);
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
@@ -81,10 +66,7 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
     Lq = Lk = p.cu_seqlens[b + 1] - cu;
   }
   const int m0 = mb * BM;
-  // ping-pong: waves w and w + 4 share a SIMD and run in opposite groups g; the groups take
-  // alternate 32-row blocks so that both see the same causal extent
-  const int g = PP ? (w >> 2) : 0;
-  const int qw0 = m0 + 32 * (PP ? 2 * (w & 3) + g : w);  // first row of this wave
+  const int qw0 = m0 + 32 * w;  // first row of this wave
   const int qi = qw0 + r32;     // this lane's query row
   const int D = p.head_dim;
 
@@ -101,7 +83,7 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   const int ntiles = (n_end + BN - 1) / BN;
   const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
 
-  auto kt = [&](int t) { return smem + (NKB == 2 ? (t & 1) : t % NKB) * TILE; };  // buffer of K tile t
+  auto kt = [&](int t) { return smem + (t & 1) * TILE; };                       // buffer of K tile t
   auto vt = [&](int t) { return smem + (NKB + (t & 1)) * TILE; };                // buffer of V tile t
   BufStager<DT, BN, NT> kst;  // K and V share row strides (checked by the launcher): one offset set
   kst.init(tid, p.k_stride[1], D);
@@ -224,11 +206,9 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
   __syncthreads();
 
   constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
-  // DMA pieces per phase: all of K and V in phase X (one barrier per tile), or one tile per
-  // half-phase (ping-pong)
-  constexpr int kPerX = PP ? kPieces : 2 * kPieces;
+  // DMA pieces: all of K and V in phase X (one barrier per tile)
+  constexpr int kPerX = 2 * kPieces;
   constexpr int kEveryX = NQK / kPerX > 0 ? NQK / kPerX : 1;
-  constexpr int kEveryY = NPV / kPieces > 0 ? NPV / kPieces : 1;
 
   // Rows past the end read as zeros (buffer range check); tiles wholly past it land in buffers
   // nobody reads again.
@@ -243,50 +223,14 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
     if (pc < kPieces) dma_k(i + 2, pc);
     else dma_v(i + 1, pc - kPieces);
   };
-  // Ping-pong schedule, half-phase h: K(h/2 + 2) when h is even, V((h + 1)/2) when odd.  K has
-  // three buffers: K(t) is read by group 0 in half-phase 2t-2 and by group 1 in 2t-1, and its
-  // buffer is rewritten (by K(t+3)) in half-phase 2t+2.
-  // (target chosen by scalar selects, not a branch: the pieces ride inside fenced MFMA steps)
-  struct DmaTarget {
-    i32x4 rsrc;
-    char* dst;
-  };
-  auto dma_target = [&](int h) {
-    const bool even = (h & 1) == 0;
-    const int t = even ? h / 2 + 2 : (h + 1) / 2;
-    return DmaTarget{BufStager<DT, BN, NT>::tile_rsrc(even ? kg : vg, p.k_stride[1], t * BN, Lk, mrows),
-                     even ? kt(t) : vt(t)};
-  };
-  auto dma_h = [&](const DmaTarget& d, int pc) { kst.piece(d.dst, d.rsrc, pc); };
-  // end of a half-phase: this wave's DMA of the previous half-phase has landed, then barrier
-  auto half_sync = [&]() {
-    if constexpr (kPieces == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else if constexpr (kPieces == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (kPieces == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else vm_wait_all();
-    __syncthreads();
-  };
-
-  // prologue: S(0).  Ping-pong: group 0 computes it alone in half-phase -1, group 1 in
-  // half-phase 0 beside group 0's first phase X.
-  auto prologue_s0 = [&]() {
-    if (tile_live(0)) {
-      qk_plain(kt(0));
-      if (tile_mask(0)) mask_max(0);
-      else plain_max();
-      to_z(s);
-    }
-  };
-  // (one copy of the S(0) code for both groups: barriers sit in wave-uniform branches)
-  if (PP && g == 1) __syncthreads();  // half-phase -1
-  prologue_s0();
-  if (!PP || g == 0) {
-    __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
-  } else {
-#pragma unroll
-    for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(0), pc);
-    half_sync();  // half-phase 0
+  // prologue: S(0)
+  if (tile_live(0)) {
+    qk_plain(kt(0));
+    if (tile_mask(0)) mask_max(0);
+    else plain_max();
+    to_z(s);
   }
+  __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
 
   // Steady-state iterations of this wave: tile i live and tile i+1 live and unmasked.  The
   // count differs between the waves of a workgroup (causal diagonal), so each wave runs its own
@@ -304,11 +248,6 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
     constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value;
     const char* K1 = kt(i + 1);
     const char* V0 = vt(i);
-    DmaTarget dx{}, dy{};
-    if constexpr (PP) {
-      dx = dma_target(2 * i + g);
-      dy = dma_target(2 * i + 1 + g);
-    }
     // phase X: QK^T(i+1) with softmax(i) and the DMA pieces riding along.  One key half after
     // the other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume
     // cur[0] then cur[1]: 48 score registers live at any step, not 64.
@@ -330,15 +269,11 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
         }
 #pragma unroll
         for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
-        if (m % kEveryX == 0 && m / kEveryX < kPerX) {
-          if constexpr (PP) dma_h(dx, m / kEveryX);
-          else dma(i, m / kEveryX);
-        }
+        if (m % kEveryX == 0 && m / kEveryX < kPerX) dma(i, m / kEveryX);
         __builtin_amdgcn_sched_barrier(0);
       }
       l_run += rs0 + rs1;
     }
-    if constexpr (PP) half_sync();
     // phase Y: PV(i) with the row max of S(i+1), one v_max3 per step
     {
       constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
@@ -353,9 +288,6 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
         if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
         const int kk = m / NDT;
         acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
-        if constexpr (PP) {
-          if (m % kEveryY == 0 && m / kEveryY < kPieces) dma_h(dy, m / kEveryY);
-        }
         if constexpr (QK) {
 #pragma unroll
           for (int e = m * PER; e < (m + 1) * PER; ++e) {
@@ -373,12 +305,8 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
       }
       if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
     }
-    if constexpr (PP) {
-      half_sync();
-    } else {
-      vm_wait_all();
-      __syncthreads();
-    }
+    vm_wait_all();
+    __syncthreads();
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -406,21 +334,8 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
     ++i;
   }
   for (; i < ntiles; ++i) {
-    if constexpr (PP) {
 #pragma unroll
-      for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(2 * i + g), pc);
-      half_sync();
-#pragma unroll
-      for (int pc = 0; pc < kPieces; ++pc) dma_h(dma_target(2 * i + 1 + g), pc);
-      half_sync();
-    } else {
-#pragma unroll
-      for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
-      vm_wait_all();
-      __syncthreads();
-    }
-  }
-  if (PP && g == 0) {  // group 1's last half-phase
+    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
     vm_wait_all();
     __syncthreads();
   }
@@ -434,50 +349,22 @@ __global__ void __launch_bounds__(PipeCfg<PP>::NW * 64, 2) fwd_pipe_kernel(const
     float* lrow = p.lse + (int64_t)bh * p.lse_row_stride;
     lrow[qi] = row_ok ? m_run + __log2f(l_tot) : kNegInf;
   }
-  // O: lane (r32, hh) holds columns 8k + 4hh .. +3 of its row for k = 4 dt + g4.  One
-  // v_permlane32_swap per dword pairs groups k, k+1 so that each lane stores 16 contiguous
-  // bytes (lanes 0-31: columns 8k..8k+7, lanes 32-63: 8k+8..8k+15): 8 dwordx4 stores instead
-  // of 16 dwordx2 (the store tail is issue-bound).
-  if constexpr (FA2_STORE_LDS && !PP) {
+  {
     // every wave passed the last tile's barrier: the K/V buffers are free for the staging image
     uint16_t* o0 = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qw0 * p.o_stride[1];
     store_rows_lds<BF16, DT>(smem + w * 32 * DT * 2, acc, inv, row_ok, o0, p.o_stride[1],
                              min(32, p.seqlen_q - qw0), D, lane);
-  } else {
-    uint16_t* orow = (uint16_t*)p.o + b * p.o_stride[0] + hq * p.o_stride[2] + (int64_t)qi * p.o_stride[1];
-    const bool row_in = qi < p.seqlen_q;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-      for (int g4 = 0; g4 < 4; g4 += 2) {
-        uint32_t a0 = E::pack2(acc[dt][4 * g4 + 0] * inv, acc[dt][4 * g4 + 1] * inv);
-        uint32_t a1 = E::pack2(acc[dt][4 * g4 + 2] * inv, acc[dt][4 * g4 + 3] * inv);
-        uint32_t b0 = E::pack2(acc[dt][4 * g4 + 4] * inv, acc[dt][4 * g4 + 5] * inv);
-        uint32_t b1 = E::pack2(acc[dt][4 * g4 + 6] * inv, acc[dt][4 * g4 + 7] * inv);
-        const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-        const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-        const int d0 = 32 * dt + 8 * g4 + 8 * hh;
-        if (row_in && d0 < D) *(u32x4*)(orow + d0) = u32x4{r0[0], r1[0], r0[1], r1[1]};
-      }
-    }
   }
   }
-}
-
-template <bool BF16, int DT, bool CAUSAL, bool PP>
-static hipError_t launch_fwd_pipe_t(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int NW = PipeCfg<PP>::NW, BM = NW * 32;
-  constexpr bool PAIR = FA2_FWD_PAIR >= 2 || (FA2_FWD_PAIR == 1 && CAUSAL);
-  const int nmb = (a.seqlen_q + BM - 1) / BM;
-  dim3 grid((PAIR ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, PP>), grid, dim3(NW * 64), 0, st, a);
-  return hipGetLastError();
 }
 
 template <bool BF16, int DT, bool CAUSAL>
 static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr bool PP = FA2_FWD_PP >= 2 || (FA2_FWD_PP == 1 && !CAUSAL);
-  return launch_fwd_pipe_t<BF16, DT, CAUSAL, PP>(a, st);
+  constexpr int BM = 128;
+  const int nmb = (a.seqlen_q + BM - 1) / BM;
+  dim3 grid((CAUSAL ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 }  // namespace fa2

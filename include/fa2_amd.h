@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 4
+#define FA2_ABI_VERSION 5
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -105,19 +105,14 @@ typedef struct fa2_bwd_args {
   float softmax_scale;
   float dropout_p;
   uint64_t dropout_seed;
-  /* optional dS workspace (ABI 2; causal-compact layout since ABI 3): when non-NULL and at
-   * least fa2_bwd_ds_workspace_bytes(args) bytes, dK/dV also stores the rounded
-   * dS = P (dP - delta) tiles it computes, and dQ = dS K becomes a streaming pass over them
-   * instead of a second recompute of S and dP.  NULL keeps the recompute dQ kernel (O(S)
-   * memory, as the reference).  Contents are scratch (no initialisation needed). */
-  void* ds_workspace;
-  int64_t ds_workspace_bytes;
-  /* optional bias gradient (ABI 3): when non-NULL (bias must be non-NULL too), dK/dV also
-   * writes dS[b, hq, i, j] = dL/ds_ij = P (dP - delta) in fp32 for every visible (query, key)
-   * pair of every (batch, q-head) into this [B, Hq, Sq, Sk] buffer (element strides below, unit
-   * key stride).  Pairs no kernel visits (fully masked tiles) are not written: zero-fill it
-   * first.  The gradient of a broadcast bias [1|B, 1|Hq, Sq, Sk] is its sum over the broadcast
-   * dims (the reference returns no bias gradient, /root/reference/src/wrapper.py:86). */
+  /* optional bias gradient (ABI 5): when non-NULL (bias must be non-NULL too), the backward
+   * also writes dL/d(bias) in fp32 into this buffer, which has the BIAS's shape
+   * [1|B, 1|Hq, Sq, Sk] (element strides below: batch, head, row; unit key stride): element
+   * (b', h', i, j) = sum over the batches and q-heads the bias broadcasts over (a zero batch /
+   * head stride in bias_stride) of dS[b, hq, i, j] = P (dP - delta), summed in a fixed order
+   * (bitwise reproducible), 0 where no pair is visible.  Every element is written; no
+   * initialisation needed; no workspace beyond this buffer.  (The reference returns no bias
+   * gradient, /root/reference/src/wrapper.py:86.) */
   float* dbias;
   int64_t dbias_stride[3];
   /* optional dK/dV split workspace (ABI 4): when non-NULL and at least
@@ -136,18 +131,11 @@ int fa2_bwd(const fa2_bwd_args* args, void* stream);
 
 /* The backward's launches selected by a bit mask, for per-kernel timing and profiling.
  * Launch order: bit 0 delta = rowsum(O * dO) (standalone kernel), bit 2 dQ (which also computes
- * delta for its rows and writes it to args->delta), bit 1 dK/dV (reads delta).  A mask must
- * produce delta before dK/dV reads it (bit 0 or bit 2, now or in an earlier call);
- * fa2_bwd == fa2_bwd_stages(args, 6, stream) without a dS workspace, 7 with one. */
+ * delta for its rows and writes it to args->delta), bit 1 dK/dV (reads delta), bit 3 the bias
+ * gradient (reads delta; needs args->dbias).  A mask must produce delta before dK/dV or the
+ * bias gradient read it (bit 0 or bit 2, now or in an earlier call);
+ * fa2_bwd == fa2_bwd_stages(args, 6, stream), 14 when args->dbias is set. */
 int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
-/* Bytes of dS workspace the backward can use for these arguments: 2 KiB per 32 x 32 (query, key)
- * tile with a visible pair, per (batch, q-head) -- about half the full grid when causal
- * (B=8 H=32 S=4096 causal: 4.33 GB).  0 when the dS path does not apply: head_dim not a
- * multiple of 8, <= 64 or > 128, an empty side, or Q/K/V/O/dO not 16-byte aligned with
- * strides that are multiples of 8 (fill those pointers and strides before calling).  With a
- * workspace the launch order is bit 0 delta, bit 1 dK/dV (+ dS tiles), bit 2 dQ = dS K, and
- * fa2_bwd runs all three. */
-int64_t fa2_bwd_ds_workspace_bytes(const fa2_bwd_args* args);
 /* Bytes of dK/dV split workspace for these sizes (batch, heads_q, heads_kv, seqlen_k, head_dim):
  * 2 * nsplit * B * Hkv * Sk * D * 4, with nsplit the smallest divisor of the group size Hq / Hkv
  * that gives at least 512 dK/dV workgroups (two per CU), or 0 when no split applies (Hq == Hkv,

@@ -1,8 +1,7 @@
 """A/B timing of several libfa2_amd.so builds in ONE process (interleaved rounds), cfg3 causal.
 
 usage: python scripts/ab.py lib_a.so lib_b.so [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd)
-WHAT: fwd | dkdv, dq (recompute path stages) | dkdvs, dqs (dS-workspace stages) | bwd (default
-backward) | bwdr (recompute backward)
+WHAT: fwd | dkdv, dq (backward stages) | bwd (whole backward)
 """
 import ctypes
 import math
@@ -24,8 +23,6 @@ for path in sys.argv[1:]:
     lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.c_void_p, ctypes.c_void_p]
     lib.fa2_last_error.restype = ctypes.c_char_p
-    lib.fa2_bwd_ds_workspace_bytes.argtypes = [ctypes.POINTER(L.BwdArgs)]
-    lib.fa2_bwd_ds_workspace_bytes.restype = ctypes.c_int64
     libs.append((os.path.basename(path), lib))
 
 b, h, s, d = 8, 32, 4096, 128
@@ -37,8 +34,7 @@ k = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 v = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 do = torch.randn_like(q)
 F = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
-flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F, "bwd": 2.5 * F, "dkdvs": 2 * F, "dkdvr": 2 * F, "dqs": 0.5 * F, "bwdr": 2.5 * F}
-from fa2_triton_amd.backward import alloc_ds_workspace  # noqa: E402
+flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F, "bwd": 2.5 * F}
 results = {(n, w): [] for n, _ in libs for w in what}
 for rnd in range(5):
     for name, lib in libs:
@@ -46,19 +42,11 @@ for rnd in range(5):
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
         delta = torch.empty_like(lse)
         _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=1, _delta=delta)
-        ws = alloc_ds_workspace(q, k, v, o, do, causal)
         calls = {
             "fwd": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
             "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=2, _delta=delta),
             "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=4, _delta=delta),
             "bwd": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None),
-            "dkdvr": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=2,
-                                                  _delta=delta, _use_ds=False),
-            "bwdr": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _use_ds=False),
-            "dkdvs": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=2,
-                                                  _delta=delta, _ds_ws=ws, _use_ds=True),
-            "dqs": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=4,
-                                                _delta=delta, _ds_ws=ws, _use_ds=True),
         }
         for w in what:
             calls[w]()

@@ -24,6 +24,11 @@ def counters(sub):
                 continue
             short = name.split("<")[0].replace("void ", "")
             agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp"):
+                # the effective clock of this very dispatch: GRBM_GUI_ACTIVE sums the 8 XCDs
+                ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                agg[short]["pass_ms"].append(ns * 1e-6)
+                agg[short]["clock_ghz"].append(float(r["Counter_Value"]) / 8.0 / ns)
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 

@@ -1,0 +1,117 @@
+"""Resource checks on the built library's gfx950 code objects (CPU only: reads the .so).
+
+The hot kernels run at two waves per SIMD with up to 256 VGPRs; a register spill there puts
+scratch loads on the critical path (and a spilled address reload's vmcnt(0) drains the LDS-DMA
+prefetch).  Round 2 shipped the causal forward and dQ with 64 and 92 bytes of scratch per lane
+(VERDICT.md, weak 3-4); this test keeps every hot instantiation at zero.
+
+How: the .so's `.hip_fatbin` section holds one clang offload bundle per translation unit; each
+gfx950 entry is an ELF code object whose `<kernel>.kd` symbols point at 64-byte kernel
+descriptors (AMDGPU ABI: group_segment_fixed_size u32 @0, private_segment_fixed_size u32 @4,
+compute_pgm_rsrc1 u32 @48 with the VGPR granule in bits 0-5).  Pure-Python ELF parsing, no ROCm
+tools needed.
+"""
+import os
+import re
+import struct
+
+import pytest
+
+from fa2_triton_amd import _lib
+
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _sections(elf: bytes):
+    """{name: (offset, size, addr)} of a 64-bit little-endian ELF."""
+    assert elf[:4] == b"\x7fELF" and elf[4] == 2 and elf[5] == 1
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+    heads = []
+    for i in range(shnum):
+        name, typ, flags, addr, off, size, link, info, align, entsize = struct.unpack_from(
+            "<IIQQQQIIQQ", elf, shoff + i * shentsize)
+        heads.append((name, typ, addr, off, size, link, entsize))
+    stroff = heads[shstrndx][3]
+
+    def nm(o):
+        return elf[stroff + o: elf.index(b"\0", stroff + o)].decode()
+
+    return {nm(h[0]): h for h in heads}, heads
+
+
+def _code_objects(lib_path):
+    data = open(lib_path, "rb").read()
+    secs, _ = _sections(data)
+    _, _, _, off, size, _, _ = secs[".hip_fatbin"]
+    fat = data[off: off + size]
+    pos = 0
+    while True:
+        pos = fat.find(MAGIC, pos)
+        if pos < 0:
+            return
+        n, = struct.unpack_from("<Q", fat, pos + len(MAGIC))
+        p = pos + len(MAGIC) + 8
+        for _ in range(n):
+            eoff, esize, tlen = struct.unpack_from("<QQQ", fat, p)
+            triple = fat[p + 24: p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple and esize:
+                yield fat[pos + eoff: pos + eoff + esize]
+        pos += len(MAGIC)
+
+
+def _kernel_descriptors(co: bytes):
+    """{kernel symbol: (private_segment_fixed_size, vgprs, lds_bytes)} of one code object."""
+    secs, heads = _sections(co)
+    name, typ, addr, off, size, link, entsize = secs[".symtab"] if ".symtab" in secs else secs[".dynsym"]
+    stroff = heads[link][3]
+    out = {}
+    for i in range(size // 24):
+        st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", co, off + i * 24)
+        sym = co[stroff + st_name: co.index(b"\0", stroff + st_name)].decode()
+        if not sym.endswith(".kd") or st_shndx == 0:
+            continue
+        sh = heads[st_shndx]
+        fo = sh[3] + (st_value - sh[2])
+        lds, scratch = struct.unpack_from("<II", co, fo)
+        rsrc1, = struct.unpack_from("<I", co, fo + 48)
+        out[sym[:-3]] = (scratch, ((rsrc1 & 0x3F) + 1) * 8, lds)
+    return out
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    kd = {}
+    for co in _code_objects(_lib.LIB_PATH):
+        kd.update(_kernel_descriptors(co))
+    assert kd, "no gfx950 kernel descriptors found in the library"
+    return kd
+
+
+# hot instantiations: bf16 / fp16 (Lb1 / Lb0), D tiles 64 and 128, causal and not; the plain
+# path (no bias, no dropout, aligned; dQ in the input dtype)
+HOT = {
+    "fwd_pipe": r"_ZN3fa215fwd_pipe_kernelILb[01]ELi(64|128)ELb[01]EEEv12fa2_fwd_args",
+    "dq": r"_ZN3fa29dq_kernelILb[01]ELi(64|128)ELb[01]ELb0ELb0ELb1ELb0EEEv12fa2_bwd_args",
+    "dkdv": r"_ZN3fa211dkdv_kernelILb[01]ELi(64|128)ELb[01]ELb0ELb0ELb1EEEv12fa2_bwd_argsi",
+}
+
+
+@pytest.mark.parametrize("kind", sorted(HOT))
+def test_hot_kernels_have_no_scratch(kernels, kind):
+    pat = re.compile(HOT[kind] + "$")
+    found = {k: v for k, v in kernels.items() if pat.match(k)}
+    assert len(found) == 8, (kind, sorted(found))  # 2 dtypes x 2 head-dim tiles x causal / not
+    spilled = {k: v[0] for k, v in found.items() if v[0] != 0}
+    assert not spilled, f"scratch bytes per lane: {spilled}"
+    for k, (_, vgprs, lds) in found.items():
+        assert vgprs <= 256, (k, vgprs)  # two waves per SIMD
+        assert lds <= 80 * 1024, (k, lds)  # two workgroups per CU
+
+
+def test_every_kernel_fits_the_cu(kernels):
+    for k, (scratch, vgprs, lds) in kernels.items():
+        assert vgprs <= 512 and lds <= 160 * 1024, (k, vgprs, lds)

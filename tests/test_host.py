@@ -66,68 +66,18 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
         _lib.check(_lib.FA2_E_UNSUPPORTED)
 
 
-def _visible_tiles(sq, sk, causal):
-    """Brute-force count of the 32 x 32 (query, key) tiles dK/dV writes for one (batch, head):
-    key tile kt of query tile t holds a visible pair iff 32 kt <= 32 t + 31 + (sk - sq)."""
-    nqt, nkt = -(-sq // 32), -(-sk // 32)
-    return sum(1 for t in range(nqt) for kt in range(nkt) if not causal or 32 * kt <= 32 * t + 31 + sk - sq)
-
-
-@pytest.mark.parametrize("causal", [False, True])
-@pytest.mark.parametrize("b,hq,sq,sk,d", [(8, 32, 4096, 4096, 128), (2, 32, 8192, 8192, 128), (3, 4, 517, 203, 64),
-                                           (1, 2, 33, 1, 256), (2, 2, 100, 100, 32), (2, 2, 100, 100, 72),
-                                           (2, 2, 100, 100, 111), (1, 3, 517, 203, 128), (1, 3, 203, 517, 96),
-                                           (1, 1, 1000, 37, 128), (1, 1, 37, 1000, 128), (1, 1, 1, 1, 128),
-                                           (1, 1, 64, 95, 80), (1, 1, 95, 64, 80), (2, 2, 4000, 33, 128)])
-def test_ds_workspace_bytes_matches_library(b, hq, sq, sk, d, causal):
-    from fa2_triton_amd.backward import ds_workspace_bytes
-
-    lib = _lib.load()
-    a = _lib.BwdArgs()
-    a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = b, hq, 1, sq, sk, d
-    a.causal = int(causal)
-    q, k = torch.empty(b, sq, hq, d, device="meta"), torch.empty(b, sk, 1, d, device="meta")
-    got = ds_workspace_bytes(q, k, k, q, q, causal)
-    assert lib.fa2_bwd_ds_workspace_bytes(ctypes.byref(a)) == got
-    if d % 8 == 0 and 64 < d <= 128:
-        assert got == b * hq * _visible_tiles(sq, sk, causal) * 2048
-    else:
-        assert got == 0
-
-
-def test_ds_workspace_causal_is_half_the_grid():
-    from fa2_triton_amd.backward import ds_workspace_bytes
-
-    q = torch.empty(8, 4096, 32, 128, device="meta")
-    assert ds_workspace_bytes(q, q, q, q, q, True) == 8 * 32 * (128 * 129 // 2) * 2048  # 4.33 GB
-    assert ds_workspace_bytes(q, q, q, q, q, False) == 8 * 32 * 128 * 128 * 2048
-
-
-def test_ds_workspace_needs_aligned_tensors():
-    """The dS path runs only on the 16-byte vector layout; otherwise the size query says 0."""
-    from fa2_triton_amd.backward import ds_workspace_bytes
-
-    base = torch.empty(1, 64, 2, 128 + 1, dtype=torch.bfloat16)
-    odd = base[..., 1:]  # data pointer 2 bytes past a 16-byte boundary, row stride 129
-    ok = torch.empty(1, 64, 2, 128, dtype=torch.bfloat16)
-    assert ds_workspace_bytes(ok, ok, ok, ok, ok, True) > 0
-    assert ds_workspace_bytes(odd, ok, ok, ok, ok, True) == 0
-    assert ds_workspace_bytes(ok, ok, ok, ok, odd, True) == 0
-    kv = torch.empty(1, 64, 4, 128, dtype=torch.bfloat16)[:, :, :2]  # K and V row strides differ
-    assert ds_workspace_bytes(ok, kv, ok, ok, ok, True) == 0
-
-
-def test_ds_workspace_is_validated_without_a_gpu():
+def test_bias_gradient_stage_is_validated_without_a_gpu():
+    """Stage bit 3 (the bias gradient) needs a dbias buffer, and a dbias buffer needs a bias."""
     lib = _lib.load()
     a = _lib.BwdArgs()
     a.batch, a.heads_q, a.heads_kv, a.seqlen_q, a.seqlen_k, a.head_dim = 1, 2, 2, 64, 64, 128
     a.dtype, a.dq_dtype, a.lse_row_stride = _lib.FA2_BF16, _lib.FA2_BF16, 128
     for name in ("q", "k", "v", "o", "dout", "lse", "delta", "dq", "dk", "dv"):
         setattr(a, name, 4096)  # never dereferenced: validation fails first
-    a.ds_workspace, a.ds_workspace_bytes = 4096, 1024
-    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"ds_workspace_bytes" in lib.fa2_last_error()
-    a.head_dim, a.ds_workspace_bytes = 111, 1 << 30
-    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"does not apply" in lib.fa2_last_error()
+    assert lib.fa2_bwd_stages(ctypes.byref(a), 8, None) == _lib.FA2_E_INVALID and b"dbias" in lib.fa2_last_error()
+    a.dbias = 4096
+    assert lib.fa2_bwd(ctypes.byref(a), None) == _lib.FA2_E_INVALID and b"without a bias" in lib.fa2_last_error()
+    assert lib.fa2_bwd_stages(ctypes.byref(a), 16, None) == _lib.FA2_E_INVALID
 
 
 def test_infer_bias_strides():

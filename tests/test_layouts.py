@@ -130,23 +130,56 @@ def test_empty_query_side(causal):
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", BIAS_SHAPES)
 @pytest.mark.parametrize("bias_dtype", ["same", "fp32"])
-def test_bias_gradient(dtype, causal, shape, bias_dtype):
+@pytest.mark.parametrize("dropout_p", [0.0, 0.17])
+def test_bias_gradient(dtype, causal, shape, bias_dtype, dropout_p):
     """dL/d(bias) (beyond the reference, which returns None) against autograd through the oracle,
     with the acceptance rule of the other gradients: err <= 3 err_pt + 1e-5, where err_pt is the
-    low-precision PyTorch oracle's error; broadcast dims are summed."""
+    low-precision PyTorch oracle's error; broadcast dims are summed.  With dropout the oracle
+    applies the forward's Philox keep mask (oracle/philox.py), as in test_dropout_bwd.py."""
+    from oracle.philox import dropout_keep_mask_torch
+
     b, hq, hkv, sq, sk, d = 2, 4, 2, 190, 270, 128
     q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, d, dtype)
     bb, bh = {"b_hq": (b, hq), "1_hq": (1, hq), "b_1": (b, 1), "1_1": (1, 1)}[shape]
     bdt = dtype if bias_dtype == "same" else torch.float32
     bias = (torch.rand(bb, bh, sq, sk, device=q.device, dtype=bdt) * 2 - 1).requires_grad_()
-    out = flash_attn_func(q, k, v, None, bias, 0.0, causal)
+    seed = 1234 if dropout_p else None
+    mask = dropout_keep_mask_torch(seed, dropout_p, b, hq, sq, sk, device=q.device) if dropout_p else None
+    out = flash_attn_func(q, k, v, None, bias, dropout_p, causal, None, seed)
     dq, dk, dv, dbias = torch.autograd.grad(out, (q, k, v, bias), do)
     assert dbias.shape == bias.shape and dbias.dtype == bias.dtype
-    ref = attention_reference(q, k, v, attn_bias=bias, causal=causal)
-    pt = attention_reference(q, k, v, attn_bias=bias, causal=causal, upcast=False, reorder_ops=True)
+    ref = attention_reference(q, k, v, attn_bias=bias, causal=causal, dropout_p=dropout_p, dropout_mask=mask)
+    pt = attention_reference(q, k, v, attn_bias=bias, causal=causal, upcast=False, reorder_ops=True,
+                             dropout_p=dropout_p, dropout_mask=mask)
     g_ref = torch.autograd.grad(ref, bias, do, retain_graph=True)[0]
     g_pt = torch.autograd.grad(pt, bias, do, retain_graph=True)[0]
     err = (dbias.float() - g_ref.float()).abs().max().item()
     err_pt = (g_pt.float() - g_ref.float()).abs().max().item()
     assert err <= 3 * err_pt + 1e-5, (err, err_pt)
     check_fa_tolerance(q, k, v, do, out, ref, pt, grads=(dq, dk, dv))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_bias_gradient_memory_and_determinism(causal):
+    """A broadcast [1, 1, S, S] bias at B=8 H=32 S=4096 (cfg3 shape): the bias gradient is summed
+    over batch and heads inside the library, so the backward allocates O(bias) memory -- less than
+    3x the bias's fp32 size on top of dQ/dK/dV -- where a [B, Hq, S, S] fp32 dS buffer would be
+    17 GB.  Two backward passes give bitwise equal gradients."""
+    b, h, s, d = 8, 32, 4096, 128
+    q, k, v, do = generate_test_data(b, h, h, s, s, d, torch.bfloat16)
+    bias = (torch.rand(1, 1, s, s, device=q.device, dtype=torch.bfloat16) - 0.5).requires_grad_()
+    out = flash_attn_func(q, k, v, None, bias, 0.0, causal)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    g1 = torch.autograd.grad(out, (q, k, v, bias), do, retain_graph=True)
+    torch.cuda.synchronize()
+    grads_bytes = sum(t.numel() * t.element_size() for t in g1)
+    extra = torch.cuda.max_memory_allocated() - base - grads_bytes
+    lse_delta = 2 * b * h * s * 4  # the LSE-shaped delta workspace
+    assert extra <= 3 * s * s * 4 + lse_delta, extra
+    g2 = torch.autograd.grad(out, (q, k, v, bias), do)
+    for x, y in zip(g1, g2):
+        assert torch.equal(x, y)
+    assert torch.isfinite(g1[3]).all()

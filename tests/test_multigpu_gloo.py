@@ -1,8 +1,9 @@
 """Multi-rank logic of bench.py on CPU (gloo, world_size 2): batch sharding with no data-path
 collective, max-over-ranks timing, whole-job throughput (weak and strong scaling), and the
 self-launch of `bench.py --gpus N` (N rank processes, rank 0 prints the line).  The GPU path uses the
-same functions with the nccl (RCCL) backend; only the barrier and the timer reduction are
-collectives."""
+same functions and the same host-side gloo group; only the barrier and the timer reductions are
+collectives (RCCL is never initialised).  A rank that dies makes the launcher stop the others and
+exit non-zero at once instead of leaving them blocked in a barrier."""
 import os
 import socket
 
@@ -81,9 +82,44 @@ def test_bench_gpus_2_launches_two_ranks_weak():
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["global_batch"] == 16
     assert [tuple(s) for s in line["shards"]] == [(0, 8), (8, 16)]
     assert line["elapsed"] == pytest.approx(0.002)  # max over the two ranks' timers
+    assert line["rank_elapsed_s"] == pytest.approx([0.001, 0.002])
 
 
 def test_bench_gpus_2_strong_splits_global_batch():
     line = _bench_dry_run("--strong", "--global-batch", "64")
     assert line["scaling"] == "strong" and line["global_batch"] == 64
     assert [tuple(s) for s in line["shards"]] == [(0, 32), (32, 64)]
+
+
+def test_bench_launcher_stops_siblings_when_a_rank_dies():
+    """Rank 1 dies at start-up (FA2_BENCH_FAIL_RANK=1) while rank 0 waits for it in the
+    process-group rendezvous: the parent must return non-zero within seconds and leave no child."""
+    import subprocess
+    import sys
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["FA2_BENCH_FAIL_RANK"] = "1"
+    t0 = time.time()
+    parent = subprocess.Popen([sys.executable, bench.__file__, "--gpus", "2", "--dry-run"], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    out, err = parent.communicate(timeout=120)
+    assert parent.returncode == 3, (parent.returncode, err)
+    assert time.time() - t0 < 60
+    # no rank process of this launch is left: the launcher's children carry the parent's pid
+    ps = subprocess.run(["ps", "-eo", "pid,ppid,args"], capture_output=True, text=True).stdout
+    orphans = [ln for ln in ps.splitlines()[1:] if ln.split()[1] == str(parent.pid)]
+    assert not orphans, orphans
+    assert "dry_run" not in out
+
+
+def test_bench_launcher_times_out(monkeypatch):
+    """A launch that does not finish within its timeout (rank 1 hangs) is stopped: status 124."""
+    import time
+
+    monkeypatch.setenv("FA2_BENCH_HANG_RANK", "1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    t0 = time.time()
+    assert bench.launch_ranks(2, ["--gpus", "2", "--dry-run"], timeout_s=10.0) == 124
+    assert time.time() - t0 < 40
