@@ -286,6 +286,8 @@ def pmc_fields(rec: dict) -> dict:
 def resolve(args):
     """Fill the workload fields left unset from the --config preset."""
     preset = CONFIGS[args.config]
+    if args.steps is None:
+        args.steps = 200 if args.config == "cfg2" else 20
     for key in ("batch", "heads", "heads_kv", "seqlen", "head_dim", "dtype"):
         if getattr(args, key) is None:
             setattr(args, key, preset[key])
@@ -300,7 +302,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg3")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; 200 for cfg2's 50 us step)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (weak scaling)")
     ap.add_argument("--strong", action="store_true", help="split --global-batch over the GPUs")

@@ -24,10 +24,20 @@
 
 namespace fa2 {
 
-template <bool BF16, int DT, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+// NW = 4: two independent workgroups per CU.  NW = 8: one workgroup of 256 rows per CU whose
+// two waves per SIMD (w and w + 4) share every K/V tile (half the LDS-DMA per MFMA); with STAG
+// the second half (waves 4-7, group B) runs half a tile behind the first: in every period between
+// two barriers group A runs [X(i) Y(i)] and group B [Y(i-1) X(i)], so each SIMD pairs one wave's
+// exponential-heavy phase X with the other's MFMA-heavy phase Y (MI355X_MICROARCH.md, "Two waves
+// per SIMD", item 9).  V then needs three buffers (group B still reads V(i-1) in period i);
+// four are kept so that the buffer index is t & 3 (with t % 3 the unrolled loop computed the
+// buffer bases at run time and spilled).
+template <bool BF16, int DT, bool CAUSAL, int NW, bool STAG>
+__global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NW = 4, NKB = 2;  // waves per workgroup, K tile buffers
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(!STAG || NW == 8, "the stagger pairs the two waves of a SIMD");
+  constexpr int NKB = 2, NVB = STAG ? 4 : 2;  // K, V tile buffers
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
@@ -38,7 +48,7 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   constexpr int EPS = 32 / NQK;      // exponentials per QK^T step
   constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
   constexpr int LEAD = 3;            // fragment reads in flight ahead of their MFMA
-  __shared__ __attribute__((aligned(16))) char smem[(NKB + 2) * TILE];  // K buffers, V0 V1
+  __shared__ __attribute__((aligned(16))) char smem[(NKB + NVB) * TILE];  // K buffers, V buffers
   static_assert(NQK % 8 == 0 && 32 % NQK == 0, "QK^T steps must carry whole pack pairs");
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
@@ -66,7 +76,9 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
     Lq = Lk = p.cu_seqlens[b + 1] - cu;
   }
   const int m0 = mb * BM;
-  const int qw0 = m0 + 32 * w;  // first row of this wave
+  // 8 waves: the two groups take alternate 32-row blocks, so both see the same causal extent
+  const int grp = NW == 8 ? (w >> 2) : 0;
+  const int qw0 = m0 + 32 * (NW == 8 ? 2 * (w & 3) + grp : w);  // first row of this wave
   const int qi = qw0 + r32;     // this lane's query row
   const int D = p.head_dim;
 
@@ -84,7 +96,7 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
 
   auto kt = [&](int t) { return smem + (t & 1) * TILE; };                       // buffer of K tile t
-  auto vt = [&](int t) { return smem + (NKB + (t & 1)) * TILE; };                // buffer of V tile t
+  auto vt = [&](int t) { return smem + (NKB + (t & (NVB - 1))) * TILE; };  // buffer of V tile t
   BufStager<DT, BN, NT> kst;  // K and V share row strides (checked by the launcher): one offset set
   kst.init(tid, p.k_stride[1], D);
   const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
@@ -206,9 +218,11 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   __syncthreads();
 
   constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
-  // DMA pieces: all of K and V in phase X (one barrier per tile)
+  // DMA pieces of a period (K and V, one barrier per tile) ride in the period's first phase:
+  // phase X for group A, phase Y for group B
   constexpr int kPerX = 2 * kPieces;
   constexpr int kEveryX = NQK / kPerX > 0 ? NQK / kPerX : 1;
+  constexpr int kEveryY = NPV / kPerX > 0 ? NPV / kPerX : 1;
 
   // Rows past the end read as zeros (buffer range check); tiles wholly past it land in buffers
   // nobody reads again.
@@ -218,7 +232,8 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   auto dma_v = [&](int t, int pc) {
     kst.piece(vt(t), BufStager<DT, BN, NT>::tile_rsrc(vg, p.v_stride[1], t * BN, Lk, mrows), pc);
   };
-  // One-barrier schedule, iteration i: K(i+2) -> the buffer of K(i), V(i+1) -> that of V(i-1).
+  // One-barrier schedule, period i: K(i+2) -> the buffer of K(i), V(i+1) -> that of V(i-1)
+  // (V(i-2) with the stagger).
   auto dma = [&](int i, int pc) {
     if (pc < kPieces) dma_k(i + 2, pc);
     else dma_v(i + 1, pc - kPieces);
@@ -232,84 +247,115 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   }
   __syncthreads();  // every wave is done with K(0) before K(2) lands in its buffer
 
-  // Steady-state iterations of this wave: tile i live and tile i+1 live and unmasked.  The
-  // count differs between the waves of a workgroup (causal diagonal), so each wave runs its own
-  // two loops; every iteration of either loop ends in the same one barrier, and the waves stay
-  // in step by iteration index.
-  int n_full = Lk / BN;  // leading tiles that need no mask for any row of this wave
-  if (CAUSAL) n_full = min(n_full, qw0 + diag + 1 >= 0 ? (qw0 + diag + 1) / BN : 0);
-  const int n_steady = max(0, min(n_full, ntiles) - 1);
-
-  // One steady iteration: softmax of the scores in cur, QK^T(i+1) into nxt.  Unrolled by two
-  // with the roles of the two score arrays swapped, so no register copies between iterations.
-  f32x16 s2[2];
-  // QK: tile i+1 is live for this wave; MASK: it needs the causal / key-tail mask.
-  auto step = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto mask_c) {
-    constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value;
+  // Phase X(i): softmax(i) of the exponent arguments in cur, QK^T(i+1) into nxt when QK (tile
+  // i+1 live for this wave), with the period's DMA pieces when DMA.  One key half after the
+  // other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume cur[0] then
+  // cur[1]: 48 score registers live at any step, not 64.
+  auto phase_x = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto dma_c, int period) {
+    constexpr bool QK = decltype(qk_c)::value, DMA = decltype(dma_c)::value;
     const char* K1 = kt(i + 1);
+    softmax_begin(cur);
+    float rs0 = 0.f, rs1 = 0.f;
+    u32x4 kf[NQK];
+    auto kfs = [&](int m) { return kfrag(K1, 2 * (m % KS) + m / KS); };
+    if constexpr (QK) {
+#pragma unroll
+      for (int j = 0; j < LEAD; ++j) kf[j] = kfs(j);
+    }
+#pragma unroll
+    for (int m = 0; m < NQK; ++m) {
+      if constexpr (QK) {
+        if (m + LEAD < NQK) kf[m + LEAD] = kfs(m + LEAD);
+        const int t = m / KS, ks = m % KS;
+        nxt[t] = E::mfma(kf[m], qf[ks], ks == 0 ? zero16() : nxt[t]);
+      }
+#pragma unroll
+      for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
+      if (DMA && m % kEveryX == 0 && m / kEveryX < kPerX) dma(period, m / kEveryX);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    l_run += rs0 + rs1;
+  };
+  // Phase Y(i): PV(i) with the row max and exponent arguments of S(i+1) in nxt when QK (masked
+  // when MASK), one v_max3 per step; the period's DMA pieces when DMA.
+  auto phase_y = [&](int i, f32x16* nxt, auto qk_c, auto mask_c, auto dma_c, int period) {
+    constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value, DMA = decltype(dma_c)::value;
     const char* V0 = vt(i);
-    // phase X: QK^T(i+1) with softmax(i) and the DMA pieces riding along.  One key half after
-    // the other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume
-    // cur[0] then cur[1]: 48 score registers live at any step, not 64.
-    {
-      softmax_begin(cur);
-      float rs0 = 0.f, rs1 = 0.f;
-      u32x4 kf[NQK];
-      auto kfs = [&](int m) { return kfrag(K1, 2 * (m % KS) + m / KS); };
+    constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
+    constexpr int PER = 32 / NPV;
+    u32x4 vf[NPV];
+    float ma = kNegInf, mb_ = kNegInf;
+    const int rel = lim_lane - (i + 1) * BN - 4 * hh;
+#pragma unroll
+    for (int j = 0; j < L; ++j) vf[j] = vfrag(V0, j);
+#pragma unroll
+    for (int m = 0; m < NPV; ++m) {
+      if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
+      const int kk = m / NDT;
+      acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
       if constexpr (QK) {
 #pragma unroll
-        for (int j = 0; j < LEAD; ++j) kf[j] = kfs(j);
-      }
-#pragma unroll
-      for (int m = 0; m < NQK; ++m) {
-        if constexpr (QK) {
-          if (m + LEAD < NQK) kf[m + LEAD] = kfs(m + LEAD);
-          const int t = m / KS, ks = m % KS;
-          nxt[t] = E::mfma(kf[m], qf[ks], ks == 0 ? zero16() : nxt[t]);
-        }
-#pragma unroll
-        for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
-        if (m % kEveryX == 0 && m / kEveryX < kPerX) dma(i, m / kEveryX);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      l_run += rs0 + rs1;
-    }
-    // phase Y: PV(i) with the row max of S(i+1), one v_max3 per step
-    {
-      constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
-      constexpr int PER = 32 / NPV;
-      u32x4 vf[NPV];
-      float ma = kNegInf, mb_ = kNegInf;
-      const int rel = lim_lane - (i + 1) * BN - 4 * hh;
-#pragma unroll
-      for (int j = 0; j < L; ++j) vf[j] = vfrag(V0, j);
-#pragma unroll
-      for (int m = 0; m < NPV; ++m) {
-        if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
-        const int kk = m / NDT;
-        acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
-        if constexpr (QK) {
-#pragma unroll
-          for (int e = m * PER; e < (m + 1) * PER; ++e) {
-            const int t = e >> 4, r = e & 15;
-            if constexpr (MASK) {
-              const int o = 32 * t + (r & 3) + 8 * (r >> 2);
-              nxt[t][r] = o < rel ? nxt[t][r] : kNegInf;
-            }
-            float& mm = t ? mb_ : ma;
-            mm = fmaxf(mm, nxt[t][r]);
-            nxt[t][r] = fmaf(nxt[t][r], sc, -m_ref);
+        for (int e = m * PER; e < (m + 1) * PER; ++e) {
+          const int t = e >> 4, r = e & 15;
+          if constexpr (MASK) {
+            const int o = 32 * t + (r & 3) + 8 * (r >> 2);
+            nxt[t][r] = o < rel ? nxt[t][r] : kNegInf;
           }
+          float& mm = t ? mb_ : ma;
+          mm = fmaxf(mm, nxt[t][r]);
+          nxt[t][r] = fmaf(nxt[t][r], sc, -m_ref);
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
+      if (DMA && m % kEveryY == 0 && m / kEveryY < kPerX) dma(period, m / kEveryY);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
+  };
+  auto sync = [&]() {
     vm_wait_all();
     __syncthreads();
   };
+  auto dma_only = [&](int period) {
+#pragma unroll
+    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(period, pc);
+  };
   using T = std::true_type;
   using F = std::false_type;
+
+  // Leading tiles that need no mask for any row of this wave, and its last live tile.  The
+  // counts differ between the waves of a workgroup (causal diagonal), so each wave runs its own
+  // loops; every period of every loop ends in the same one barrier, and the waves stay in step by
+  // period index.
+  int n_full = Lk / BN;
+  if (CAUSAL) n_full = min(n_full, qw0 + diag + 1 >= 0 ? (qw0 + diag + 1) / BN : 0);
+  int last = -1;  // last live tile of this wave
+  if (ntiles > 0 && tile_live(0)) {
+    last = ntiles - 1;
+    if (CAUSAL) last = min(last, (qw0 + 31 + diag) / BN);
+  }
+  // One period: X(i) then Y(i).  Group A ends the period after Y(i); with the stagger group B
+  // ends it between X(i) and Y(i), so B's Y(i) runs in the next period beside A's X(i+1): every
+  // wave passes the same number of barriers, B half a tile later.
+  const bool late = STAG && grp == 1;
+  // The conditional barrier is one asm statement (the branch around s_barrier is inside it): as
+  // an if() around __syncthreads() it split the period into basic blocks and the compiler spilled.
+  const uint32_t late_s = __builtin_amdgcn_readfirstlane(late ? 1u : 0u);
+  auto bar_if = [&](uint32_t flag) {
+    asm volatile(
+        "s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_barrier\n1:"
+        :: "s"(flag) : "memory", "scc");
+  };
+  auto step = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto mask_c) {
+    phase_x(i, cur, nxt, qk_c, T{}, i);
+    if constexpr (STAG) bar_if(late_s);
+    phase_y(i, nxt, qk_c, mask_c, F{}, i);
+    if constexpr (STAG) bar_if(late_s ^ 1u);
+    else sync();
+  };
+  // steady periods (tile i+1 live and unmasked) unrolled by two with the roles of the two score
+  // arrays swapped, so no register copies between periods
+  f32x16 s2[2];
+  const int n_steady = max(0, min(n_full, ntiles) - 1);
   int i = 0;
   for (; i + 1 < n_steady; i += 2) {
     step(i, s, s2, T{}, F{});
@@ -321,24 +367,22 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
     s[1] = s2[1];
     ++i;
   }
-
-  // Tail of this wave: next tile on the diagonal / key tail (pipelined, masked), this wave's
-  // last live tile (softmax + PV only), then tiles past its diagonal (DMA + barrier only).
-  for (; i < ntiles && tile_live(i) && tile_live(i + 1); ++i) {
+  // tail: next tile on the diagonal / key tail (masked), the last live tile (softmax + PV only),
+  // then tiles past the diagonal (DMA + barrier only)
+  for (; i < last; ++i) {
     step(i, s, s2, T{}, T{});
     s[0] = s2[0];
     s[1] = s2[1];
   }
-  if (i < ntiles && tile_live(i)) {
+  if (i == last) {
     step(i, s, s2, F{}, F{});
     ++i;
   }
   for (; i < ntiles; ++i) {
-#pragma unroll
-    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(i, pc);
-    vm_wait_all();
-    __syncthreads();
+    dma_only(i);
+    sync();
   }
+  if (STAG) __syncthreads();  // group B's last phase Y reads a V buffer the epilogue reuses
   vm_wait_all();
 
   // ---- epilogue ----------------------------------------------------------------------------
@@ -358,12 +402,21 @@ __global__ void __launch_bounds__(256, 2) fwd_pipe_kernel(const fa2_fwd_args p) 
   }
 }
 
+#ifndef FA2_FWD_NW
+#define FA2_FWD_NW 4
+#endif
+#ifndef FA2_FWD_STAG
+#define FA2_FWD_STAG 0
+#endif
+
 template <bool BF16, int DT, bool CAUSAL>
 static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int BM = 128;
+  constexpr int NW = FA2_FWD_NW;
+  constexpr bool STAG = NW == 8 && FA2_FWD_STAG;
+  constexpr int BM = NW * 32;
   const int nmb = (a.seqlen_q + BM - 1) / BM;
   dim3 grid((CAUSAL ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, NW, STAG>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
 

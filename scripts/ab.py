@@ -1,6 +1,6 @@
 """A/B timing of several libfa2_amd.so builds in ONE process (interleaved rounds), cfg3 causal.
 
-usage: python scripts/ab.py lib_a.so lib_b.so [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd)
+usage: python scripts/ab.py lib_a.so lib_b.so [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd, SHAPE=B,H,S,D)
 WHAT: fwd | dkdv, dq (backward stages) | bwd (whole backward)
 """
 import ctypes
@@ -25,7 +25,7 @@ for path in sys.argv[1:]:
     lib.fa2_last_error.restype = ctypes.c_char_p
     libs.append((os.path.basename(path), lib))
 
-b, h, s, d = 8, 32, 4096, 128
+b, h, s, d = (int(x) for x in os.environ.get("SHAPE", "8,32,4096,128").split(","))  # B, H, S, D
 causal = os.environ.get("CAUSAL", "1") == "1"
 what = os.environ.get("WHAT", "fwd,dkdv,dq").split(",")
 torch.manual_seed(0)

@@ -7,7 +7,7 @@ uses relative imports, so nothing is rewritten; what is copied is the Python hos
 sources with their build script, the C ABI header (into the package's include/, where build.py
 finds it) and the built gfx950 library when present -- the oracle and tests stay behind.
 
-usage: python scripts/export_to_liger.py LIGER_CHECKOUT [--no-lib]
+usage: python scripts/export_to_liger.py LIGER_CHECKOUT [--no-lib] [--force]
 then:  import liger_kernel.ops.flash_attention as fa; fa.flash_attn_func(q, k, v, causal=True)
        (rebuild in place with `python -m liger_kernel.ops.flash_attention.build` if needed)
 """
@@ -21,12 +21,25 @@ PKG = os.path.join(ROOT, "fa2_triton_amd")
 FA_DIR_IN_LIGER = os.path.join("src", "liger_kernel", "ops", "flash_attention")
 
 
-def export(liger_root: str, with_lib: bool = True) -> list:
+MANIFEST = ".fa2_export_manifest"
+
+
+def export(liger_root: str, with_lib: bool = True, force: bool = False) -> list:
+    """Copy the package into the checkout.  A directory left by an earlier export (it holds the
+    manifest of the files that export wrote) is refreshed: exactly those files are removed first,
+    anything else in it is kept.  A directory without a manifest is someone else's: refused
+    unless `force`, and even then only overwritten file by file, never deleted."""
     dst = os.path.join(liger_root, FA_DIR_IN_LIGER)
-    if os.path.exists(dst):
-        shutil.rmtree(dst)
-    os.makedirs(os.path.join(dst, "csrc"))
-    os.makedirs(os.path.join(dst, "include"))
+    manifest = os.path.join(dst, MANIFEST)
+    if os.path.exists(manifest):
+        for rel in open(manifest).read().split():
+            path = os.path.join(dst, rel)
+            if os.path.isfile(path):
+                os.remove(path)
+    elif os.path.exists(dst) and os.listdir(dst) and not force:
+        raise SystemExit(f"{dst} exists and was not written by this script; pass --force to overwrite files in it")
+    os.makedirs(os.path.join(dst, "csrc"), exist_ok=True)
+    os.makedirs(os.path.join(dst, "include"), exist_ok=True)
     written = []
     for name in sorted(os.listdir(PKG)):
         if name.endswith(".py") or (with_lib and name == "libfa2_amd.so"):
@@ -38,6 +51,8 @@ def export(liger_root: str, with_lib: bool = True) -> list:
             written.append(os.path.join(dst, "csrc", name))
     shutil.copy2(os.path.join(ROOT, "include", "fa2_amd.h"), os.path.join(dst, "include", "fa2_amd.h"))
     written.append(os.path.join(dst, "include", "fa2_amd.h"))
+    with open(manifest, "w") as f:
+        f.write("\n".join(os.path.relpath(p, dst) for p in written) + "\n")
     return written
 
 
@@ -45,8 +60,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("liger_root")
     ap.add_argument("--no-lib", action="store_true", help="do not copy the built libfa2_amd.so")
+    ap.add_argument("--force", action="store_true", help="overwrite files in a directory this script did not write")
     args = ap.parse_args(argv)
-    for path in export(args.liger_root, not args.no_lib):
+    for path in export(args.liger_root, not args.no_lib, args.force):
         print(path)
 
 

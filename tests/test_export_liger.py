@@ -32,3 +32,19 @@ def test_export_imports_as_liger_op(tmp_path):
     env = {k: v for k, v in os.environ.items() if k != "FA2_AMD_LIB"}
     res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=str(tmp_path))
     assert res.returncode == 0 and "ok" in res.stdout, res.stderr
+
+
+def test_export_never_deletes_foreign_files(tmp_path):
+    """A re-export refreshes only the files its manifest lists; a directory the script did not
+    write is refused without --force (the old export ran rmtree on it)."""
+    script = os.path.join(ROOT, "scripts", "export_to_liger.py")
+    dst = tmp_path / "src" / "liger_kernel" / "ops" / "flash_attention"
+    dst.mkdir(parents=True)
+    (dst / "mine.py").write_text("x = 1\n")
+    res = subprocess.run([sys.executable, script, str(tmp_path), "--no-lib"], capture_output=True, text=True)
+    assert res.returncode != 0 and "--force" in res.stderr
+    subprocess.run([sys.executable, script, str(tmp_path), "--no-lib", "--force"], check=True, capture_output=True)
+    assert (dst / "mine.py").read_text() == "x = 1\n" and (dst / "wrapper.py").exists()
+    (dst / "wrapper.py").write_text("stale\n")
+    subprocess.run([sys.executable, script, str(tmp_path), "--no-lib"], check=True, capture_output=True)
+    assert (dst / "mine.py").exists() and (dst / "wrapper.py").read_text() != "stale\n"

@@ -67,9 +67,7 @@ def test_dkv_workspace_is_validated_without_a_gpu():
 
 CASES = [
     # b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype
-    # MQA, dS path.  (bf16 at Sq = Sk = 777 causal misses the rule by one bf16 ulp on the largest
-    # dV element, -16.5 vs -16.625, with and without the split alike -- bit-identical dV, since
-    # one q-head per split sums in the same order; scripts/diag_split.py.  fp16 here.)
+    # MQA (the bf16 twin of the first case is the xfail below)
     (1, 16, 1, 777, 777, 128, True, 0.0, False, False, torch.float16),
     (1, 16, 1, 777, 901, 128, False, 0.0, False, False, torch.bfloat16),
     (2, 8, 2, 1000, 1000, 64, True, 0.0, False, False, torch.bfloat16),   # GQA, recompute path
@@ -85,6 +83,15 @@ CASES = [
 def test_split_matches_oracle(b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype):
     assert _expected_split(b, hq, hkv, sk) > 1
     run_case(b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtype, forward_only=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.xfail(strict=True, reason="bf16 MQA Sq=Sk=777 causal: the largest dV element rounds to -16.625 "
+                   "where the fp32 oracle gives -16.5, one bf16 ulp over the reference rule, with and without "
+                   "the q-head split alike (bit-identical dV: one q-head per split sums in the same order; "
+                   "scripts/diag_split.py).  Kept visible rather than switched to fp16 (ADVICE r02).")
+def test_split_mqa_777_causal_bf16():
+    run_case(1, 16, 1, 777, 777, 128, True, 0.0, False, False, torch.bfloat16, forward_only=False)
 
 
 @pytest.mark.gpu
