@@ -85,9 +85,16 @@ __global__ void __launch_bounds__(256) delta_kernel(const fa2_bwd_args p) {
 // the group's q-heads are dealt to nsplit workgroups per key block, each writes its fp32 partial
 // dK/dV sums to p.dkv_workspace ([nsplit][B][Hkv][Sk][D], unscaled) and dkv_reduce_kernel adds
 // them in split order (deterministic).
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
+// BIASK as dq_kernel: 0 none, 1 element loads from global memory, 16 / 17 a 16-bit bias with
+// 16-byte aligned rows staged per wave by LDS-DMA: [32 query rows x 32 keys] of the step (2 KiB,
+// single buffered), read with the transposing ds_read_b64_tr_b16 straight into the register
+// order of the S accumulator (key on the lane).  The tile of step j+1 goes out as soon as step j
+// has formed P, so it lands under the dV / dK chains (the step's closing wait covers it).
+template <bool BF16, int DT, bool CAUSAL, int BIASK, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_bwd_args p, int nsplit) {
   using E = Elem<BF16>;
+  constexpr bool BIAS = BIASK != 0, BIASL = BIASK >= 16;
+  constexpr int kBiasKTile = 32 * 32 * 2;  // one wave's [32 rows][32 keys] bias tile
   constexpr int NT = 256;
   constexpr int BNK = 128;          // keys per workgroup
   constexpr int BMQ = 32;           // query rows per tile
@@ -96,7 +103,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   constexpr int VT = BNK * DT * 2;  // V tile bytes
   constexpr int QT = BMQ * DT * 2;  // Q (or dO) tile bytes
   constexpr int ST = 2 * BMQ * 4;   // LSE2 + delta rows of a tile
-  __shared__ __attribute__((aligned(16))) char smem[VT + 4 * QT + 2 * ST];
+  __shared__ __attribute__((aligned(16))) char smem[VT + 4 * QT + 2 * ST + (BIASL ? 4 * kBiasKTile : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -228,6 +235,32 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
   };
 
+  // this wave's bias tiles (BIASL): [32 query rows from m][32 keys from kw0] of step (hq, m)
+  using BiasStager = BufStager<32, 32, 64>;
+  BiasStager bst;
+  int brows = 0;
+  char* const bwk = smem + VT + 4 * QT + 2 * ST + w * kBiasKTile;
+  if constexpr (BIASL) {
+    bst.init(lane, p.bias_stride[2], 32);
+    brows = BiasStager::max_rows(p.bias_stride[2]);
+  }
+  auto bias_issue = [&](int hq_, int m_) {
+    if constexpr (BIASL) {
+      const uint16_t* bg = (const uint16_t*)p.bias + b * p.bias_stride[0] + hq_ * p.bias_stride[1] + kw0;
+      const i32x4 r = BiasStager::tile_rsrc(bg, p.bias_stride[2], m_, p.seqlen_q, brows);
+#pragma unroll
+      for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bwk, r, it);
+    }
+  };
+  // the bias of register i (query row m + (i & 3) + 8 (i >> 2) + 4 hh, this lane's key): element
+  // i & 7 of transposed read i >> 3
+  auto bias_rd = [&](int half) -> u32x4 { return lds_tr_frag<32, 32>(bwk, 16 * half, 0, lane); };
+  auto bias_of = [&](const u32x4* bt2, int i) -> float {
+    const int j = i & 7;
+    const u32x2 pair = {bt2[i >> 3][(j >> 2) * 2], bt2[i >> 3][(j >> 2) * 2 + 1]};
+    return bias_elem<BIASK>(pair, j & 3);
+  };
+
   u32x4 kf[KS];
   {
     const uint16_t* krow = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2] + (int64_t)(kval ? kj : 0) * p.k_stride[1];
@@ -239,6 +272,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     stage_tile<DT, BNK, NT, ALIGNED>(Vs, vg, p.v_stride[1], n0, Lk, D, tid);
     if constexpr (ALIGNED) stage_desc(0);
     else stage(0);
+    bias_issue(h0, tile_row(0));
   }
   f32x16 dk[NDT], dv[NDT];
 #pragma unroll
@@ -247,9 +281,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
 
   // Phases (sched_barrier-separated so each phase's LDS fragments stay inside it and the
   // register peak stays under 256): S, dP -> P, dS -> dV, dK.
-  auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m) {
+  auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m, auto next_bias) {
     constexpr bool MASK = decltype(mask_c)::value;
     f32x16 s = zero16(), dp = zero16();
+    u32x4 bt2[2];
+    if constexpr (BIASL) {
+      bt2[0] = bias_rd(0);
+      bt2[1] = bias_rd(1);
+    }
     {
       // fenced steps: the S chain (one fragment per MFMA, read kDkdvLS MFMAs ahead), then the dP
       // chain (two fragments per MFMA, kDkdvLD ahead): deeper prefetch than alternating chains
@@ -305,7 +344,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         const int i = 4 * g4 + j;
         const int o = j + 8 * g4;
         float x = s[i];
-        if (BIAS) {
+        if constexpr (BIASL) {
+          x = fmaf(x, scale2, kLog2e * bias_of(bt2, i));
+        } else if constexpr (BIAS) {
           const int qr = m + o + 4 * hh;
           const int qc = qr < Lq ? qr : Lq - 1;
           const int kc = kval ? kj : Lk - 1;
@@ -332,6 +373,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       dsp[g4 >> 1][2 * (g4 & 1) + 0] = E::pack2(dsv[0], dsv[1]);
       dsp[g4 >> 1][2 * (g4 & 1) + 1] = E::pack2(dsv[2], dsv[3]);
     }
+    next_bias();  // this step's bias tile is consumed: the next one may land in its buffer
     __builtin_amdgcn_sched_barrier(0);
     {
       // steps m: dt = m % NDT (independent chains back to back), r = m / NDT: (sp, dV | dK);
@@ -361,8 +403,23 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   // The dP accumulator starts at -delta (the delta workspace holds -rowsum(O dO)), so the chain
   // yields dP - delta and dS is one multiply; the LSE2 and -delta rows are read from LDS at the
   // start of the step, long before their use.
-  auto body_pipe = [&](auto mask_c, const char* Q, const char* O, const char* S, int m) {
+  auto body_pipe = [&](auto mask_c, const char* Q, const char* O, const char* S, int m, auto next_bias) {
     constexpr bool MASK = decltype(mask_c)::value;
+    // A bias (BIASL) enters as the S chain's initial accumulator together with the LSE2 rows,
+    // b / scale - LSE2 / (scale log2 e): the chain yields x with P = exp2(x scale log2 e), so the
+    // P phase needs neither the bias nor the LSE2 registers (at the 256-register limit both spilled
+    // there, and the spilled DMA offsets' reloads drained the Q / dO prefetch).
+    f32x16 binit;
+    if constexpr (BIASL) {
+      const u32x4 bt2[2] = {bias_rd(0), bias_rd(1)};
+      const float rs = 1.f / scale, rl = -1.f / scale2;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 lg = *(const f32x4*)(S + 4 * (8 * g4 + 4 * hh));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) binit[4 * g4 + j] = fmaf(bias_of(bt2, 4 * g4 + j), rs, lg[j] * rl);
+      }
+    }
     constexpr int LS = kDkdvLS < KS ? kDkdvLS : KS, LD = kDkdvLD < KS ? kDkdvLD : KS;
     constexpr int EP = 16 / KS;          // P elements per dP step
     constexpr int N = 4 * NDT;           // dV / dK steps
@@ -393,12 +450,13 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
         if ((KS >= 4 ? ks == KS - 4 + g4 : ks == KS - 2 + g4 / 2)) rd_nd(g4);
       // LSE group g4 is first used at dP step 4 g4 / EP and read one step ahead; the groups
       // needed in dP step 0 are read here
-      if (ks == KS - 1) {
+      if (!BIASL && ks == KS - 1) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
           if ((4 * g4) / EP == 0) rd_lse(g4);
       }
-      s = E::mfma(fq[ks], kf[ks], ks == 0 ? zero16() : s);
+      if constexpr (BIASL) s = E::mfma(fq[ks], kf[ks], ks == 0 ? binit : s);
+      else s = E::mfma(fq[ks], kf[ks], ks == 0 ? zero16() : s);
       __builtin_amdgcn_sched_barrier(0);
     }
     int lo = 0, hi = 0;  // as in body(): the visible row window of this lane's key
@@ -414,7 +472,9 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     u32x4 pp[2], dsp[2];
     auto p_elem = [&](int i) {  // P in place of S, packed pairwise
       const int o = (i & 3) + 8 * (i >> 2);
-      float pr = __builtin_amdgcn_exp2f(fmaf(s[i], sc, -l4[i >> 2][i & 3]));
+      float pr;
+      if constexpr (BIASL) pr = __builtin_amdgcn_exp2f(s[i] * scale2);
+      else pr = __builtin_amdgcn_exp2f(fmaf(s[i], sc, -l4[i >> 2][i & 3]));
       if (MASK) pr = (o >= lo && o < hi) ? pr : 0.f;
       s[i] = pr;
     };
@@ -433,7 +493,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       for (int e = ks * EP; e < (ks + 1) * EP; ++e) p_elem(e);
 #pragma unroll
       for (int g4 = 1; g4 < 4; ++g4)
-        if ((4 * g4) / EP > 0 && ks == (4 * g4) / EP - 1) rd_lse(g4);
+        if (!BIASL && (4 * g4) / EP > 0 && ks == (4 * g4) / EP - 1) rd_lse(g4);
       __builtin_amdgcn_sched_barrier(0);
     }
     auto ds_elem = [&](int i) {  // dS = P (dP - delta) in place of dP, packed pairwise
@@ -447,6 +507,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       const int dt = mm % NDT, r = mm / NDT;
       return lds_tr_frag<DT, BMQ>((r & 1) ? Q : O, 16 * (r >> 1), 32 * dt, lane);
     };
+    next_bias();  // P is formed: the next step's bias tile may land in this wave's buffer
 #pragma unroll
     for (int j = 0; j < LT; ++j) fr[j] = rd(j);
     p_pack(0);
@@ -491,18 +552,27 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     // wave-uniform tile class
     const bool dead = kw0 >= Lk || (CAUSAL && kw0 > m + BMQ - 1 + diag);
     const bool need_mask = (m + BMQ > Lq) || (kw0 + 31 >= Lk) || (CAUSAL && kw0 + 31 > m + diag);
+    // the bias tile of the next step (BIASL), issued once this step's P no longer needs the buffer
+    auto next_bias = [&]() {
+      if (step + 1 < total) {
+        const bool wrap = mt + 1 == n_mt;
+        bias_issue(hq + (wrap ? 1 : 0), tile_row(wrap ? 0 : mt + 1));
+      }
+    };
     if (!dead) {
-      if constexpr (!BIAS && !DROPOUT) {
+      if constexpr ((!BIAS || BIASL) && !DROPOUT) {
         if (need_mask)
-          body_pipe(std::true_type{}, qt(cur), ot(cur), st(cur), m);
+          body_pipe(std::true_type{}, qt(cur), ot(cur), st(cur), m, next_bias);
         else
-          body_pipe(std::false_type{}, qt(cur), ot(cur), st(cur), m);
+          body_pipe(std::false_type{}, qt(cur), ot(cur), st(cur), m, next_bias);
       } else {
         if (need_mask)
-          body(std::true_type{}, qt(cur), ot(cur), st(cur), hq, m);
+          body(std::true_type{}, qt(cur), ot(cur), st(cur), hq, m, next_bias);
         else
-          body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m);
+          body(std::false_type{}, qt(cur), ot(cur), st(cur), hq, m, next_bias);
       }
+    } else {
+      next_bias();
     }
     vm_wait_all();
     __syncthreads();
@@ -638,19 +708,26 @@ struct DqCfg {
 // LDS (double buffered).  Per tile and wave:
 //   S^T, dP^T [key][q]   2 x (8 + 8) MFMA (A = K / V row fragments, B = Q / dO in VGPRs)
 //   dQ^T[d][q] += K^T dS^T   NDT*4 MFMA (A = K^T via ds_read_b64_tr_b16)
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED, bool DQF32>
+// BIASK: 0 no bias; 1 any bias, read element by element from global memory; 16 / 17 an fp16 /
+// bf16 bias with 16-byte aligned rows, staged per wave by LDS-DMA like the forward's
+// (fwd_pipe_kernel.h): each wave's [32 rows x 64 keys] bias tile of tile i goes out first at the
+// top of tile i and is waited for (counted vmcnt, the next K/V tile left in flight) right before
+// the softmax gradient of its first key half.
+template <bool BF16, int DT, bool CAUSAL, int BIASK, bool DROPOUT, bool ALIGNED, bool DQF32>
 __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) dq_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
+  constexpr bool BIAS = BIASK != 0, BIASL = BIASK >= 16;
   constexpr int NW = DqCfg<DT>::NW;
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32, BN = 64;
   constexpr int KS = DT / 16;
   constexpr int NDT = DT / 32;
   constexpr int TILE = BN * DT * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + (BIASL ? NW * kBiasTile : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
+  char* const bw = smem + 4 * TILE + w * kBiasTile;  // this wave's bias tile (BIASL)
   // work items head-major per XCD (xcd_item), heaviest first; under a causal mask a workgroup runs
   // a mirrored pair of row blocks of one head (nmb-1-j, then j: equal causal work per workgroup)
   const int nmb = (p.seqlen_q + BM - 1) / BM;
@@ -701,6 +778,42 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
       stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, Lk, D, tid);
       stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, Lk, D, tid);
     }
+  };
+  // this wave's bias tiles (BIASL): [32 rows from mw0][64 keys], rows past seqlen_q read as zeros
+  using BiasStager = BufStager<64, 32, 64>;
+  BiasStager bst;
+  const uint16_t* bg = nullptr;
+  int brows = 0;
+  if constexpr (BIASL) {
+    int ln = lane;  // opaque: the offsets are not hoisted out of the item loop (spilled across it)
+    asm volatile("" : "+v"(ln));
+    bst.init(ln, p.bias_stride[2], 64);
+    brows = BiasStager::max_rows(p.bias_stride[2]);
+    bg = (const uint16_t*)p.bias + b * p.bias_stride[0] + hq * p.bias_stride[1];
+  }
+  auto bias_issue = [&](int n) {
+    if constexpr (BIASL) {
+      const i32x4 r = BiasStager::tile_rsrc(bg + n, p.bias_stride[2], mw0, p.seqlen_q, brows);
+#pragma unroll
+      for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bw, r, it);
+    }
+  };
+  // bias of the current tile landed; `later` (the next K/V tile's pieces) may stay in flight
+  constexpr int kKV = 2 * BufStager<DT, BN, NT>::kIters;
+  auto bias_wait = [&](bool later) {
+    if constexpr (BIASL) {
+      if (later) {
+        if constexpr (kKV == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if constexpr (kKV == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else vm_wait_all();
+      } else {
+        vm_wait_all();
+      }
+    }
+  };
+  auto bias_frag = [&](int h, int g) -> u32x2 {
+    if constexpr (BIASL) return bias_tile_frag(bw, r32, hh, h, g);
+    else return u32x2{0u, 0u};
   };
   if (ntiles > 0) stage_kv(0, 0);
 
@@ -760,9 +873,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 
   // one 64-key tile: S^T and dP^T for both 32-key halves first, then the softmax-gradient
   // VALU of each half beside the other half's MFMAs, then dQ^T += K^T dS^T.
-  auto tile = [&](auto mask_c, const char* K, const char* V, int n0) {
+  auto tile = [&](auto mask_c, const char* K, const char* V, int n0, bool later) {
     constexpr bool MASK = decltype(mask_c)::value;
     const int rel = lim_lane - n0 - 4 * hh;
+    bias_wait(later);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (MASK && !(n0 + 32 * t < Lk && (!CAUSAL || n0 + 32 * t <= mw0 + 31 + diag))) continue;
@@ -794,7 +908,9 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           const int i = 8 * sp + j;
           const int o = 32 * t + (i & 3) + 8 * (i >> 2);
           float x = s[i];
-          if (BIAS) {
+          if constexpr (BIASL) {
+            x = fmaf(x, scale2, kLog2e * bias_elem<BIASK>(bias_frag(t, i >> 2), i & 3));
+          } else if constexpr (BIAS) {
             const int kj = n0 + o + 4 * hh;
             const int kc = kj < Lk ? kj : Lk - 1;
             const int qc = qvalid ? qi : 0;
@@ -836,14 +952,21 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   // the same wave:
   //   [S, dP of half 0] [S, dP of half 1 | dS of half 0] [dQ of half 0 | dS 0-7 of half 1]
   //   [dQ of half 1 | dS 8-15 of half 1 beside its first steps]
-  auto tile_pipe = [&](const char* K, const char* V) {
+  auto tile_pipe = [&](const char* K, const char* V, bool later) {
     constexpr int L = kDqPipeLead;  // two score pairs live: one step of fragments in flight
     f32x16 s[2], dp[2];
     u32x4 dsp[2][2];
+    u32x2 bz[2];  // bias of the current 4-key group (BIASL), read one element group ahead
     // dS of element e (0..15) of half t -> packed pair in dsp[t]
     float dsv_lo = 0.f;
     auto ds_elem = [&](int t, int e) {
-      const float pr = __builtin_amdgcn_exp2f(fmaf(s[t][e], sc, nlse));
+      float x = s[t][e], u = sc;
+      if constexpr (BIASL) {
+        if ((e & 3) == 0) bz[t] = bias_frag(t, e >> 2);
+        x = fmaf(x, p.softmax_scale, bias_elem<BIASK>(bz[t], e & 3));
+        u = kLog2e;
+      }
+      const float pr = __builtin_amdgcn_exp2f(fmaf(x, u, nlse));
       const float d = pr * (dp[t][e] - del_i);
       if (e & 1) dsp[t][e >> 3][(e & 7) >> 1] = E::pack2(dsv_lo, d);
       else dsv_lo = d;
@@ -885,6 +1008,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     };
     constexpr int SDP_STEPS = 2 * KS, DQ_STEPS = 2 * NDT;
     sdp(0, [](int) {});
+    bias_wait(later);
     sdp(1, [&](int st) {  // 16 dS elements of half 0 over the S/dP steps of half 1
 #pragma unroll
       for (int e = st * 16 / SDP_STEPS; e < (st + 1) * 16 / SDP_STEPS; ++e) ds_elem(0, e);
@@ -909,16 +1033,19 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   for (int it = 0; it < ntiles; ++it) {
     const int cur = it & 1;
     const int n0 = it * BN;
-    if (it + 1 < ntiles) stage_kv(cur ^ 1, n0 + BN);
     const bool dead = CAUSAL && (n0 > mw0 + 31 + diag);
+    // (the bias tile first: its counted wait leaves the next K/V tile in flight)
+    if (!dead) bias_issue(n0);
+    const bool later = it + 1 < ntiles;
+    if (later) stage_kv(cur ^ 1, n0 + BN);
     const bool need_mask = (n0 + BN > Lk) || (mw0 + 31 >= Lq) || (CAUSAL && n0 + BN - 1 > mw0 + diag);
     if (!dead) {
       if (need_mask)
-        tile(std::true_type{}, kt(cur), vt(cur), n0);
-      else if constexpr (!BIAS && !DROPOUT)
-        tile_pipe(kt(cur), vt(cur));
+        tile(std::true_type{}, kt(cur), vt(cur), n0, later);
+      else if constexpr ((!BIAS || BIASL) && !DROPOUT)
+        tile_pipe(kt(cur), vt(cur), later);
       else
-        tile(std::false_type{}, kt(cur), vt(cur), n0);
+        tile(std::false_type{}, kt(cur), vt(cur), n0, later);
     }
     vm_wait_all();
     __syncthreads();
@@ -1164,10 +1291,24 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     constexpr bool PAIR = CAUSAL;
     const int nmb = (a.seqlen_q + BM - 1) / BM;
     dim3 grid((PAIR ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
-    if (a.dq_dtype == FA2_F32)
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
-    else
-      hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
+    auto dq = [&](auto biask_c) {
+      constexpr int BK = decltype(biask_c)::value;
+      if (a.dq_dtype == FA2_F32)
+        hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BK, DROPOUT, ALIGNED, true>), grid, dim3(NW * 64), 0, st, a);
+      else
+        hipLaunchKernelGGL((dq_kernel<BF16, DT, CAUSAL, BK, DROPOUT, ALIGNED, false>), grid, dim3(NW * 64), 0, st, a);
+    };
+    if constexpr (!BIAS) {
+      dq(std::integral_constant<int, 0>{});
+    } else if constexpr (ALIGNED) {
+      // a 16-bit bias with 16-byte aligned rows: LDS-staged bias tiles
+      if (bias16_rows(a.bias, a.bias_dtype, a.bias_stride))
+        a.bias_dtype == FA2_BF16 ? dq(std::integral_constant<int, 17>{}) : dq(std::integral_constant<int, 16>{});
+      else
+        dq(std::integral_constant<int, 1>{});
+    } else {
+      dq(std::integral_constant<int, 1>{});
+    }
   }
   if ((stages & 8) && BIAS && a.dbias && a.seqlen_q > 0 && a.seqlen_k > 0) {
     const int bb = a.bias_stride[0] != 0 ? a.batch : 1, hb = a.bias_stride[1] != 0 ? a.heads_q : 1;
@@ -1178,7 +1319,20 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   if ((stages & 2) && a.seqlen_k > 0) {
     const int ns = dkv_split(a);
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
-    hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a, ns);
+    auto dkdv = [&](auto biask_c) {
+      constexpr int BK = decltype(biask_c)::value;
+      hipLaunchKernelGGL((dkdv_kernel<BF16, DT, CAUSAL, BK, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a, ns);
+    };
+    if constexpr (!BIAS) {
+      dkdv(std::integral_constant<int, 0>{});
+    } else if constexpr (ALIGNED) {
+      if (bias16_rows(a.bias, a.bias_dtype, a.bias_stride))
+        a.bias_dtype == FA2_BF16 ? dkdv(std::integral_constant<int, 17>{}) : dkdv(std::integral_constant<int, 16>{});
+      else
+        dkdv(std::integral_constant<int, 1>{});
+    } else {
+      dkdv(std::integral_constant<int, 1>{});
+    }
     launch_dkv_reduce<BF16>(a, ns, st);
   }
   return hipGetLastError();

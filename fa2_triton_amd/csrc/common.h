@@ -87,6 +87,27 @@ FA2_DEV float load_bias(const void* base, int64_t idx, int code) {
   return code == 17 ? Elem<true>::to_f32(x) : Elem<false>::to_f32(x);
 }
 
+// 16-bit bias tiles (BIASK 16: fp16, 17: bf16) of one wave: [32 rows][64 keys] staged by LDS-DMA
+// in the Tile<64, 32> image (BufStager<64, 32, 64>).  Lane (r32, hh) of a swapped S^T accumulator
+// holds keys 32 h + 8 g + 4 hh + (0..3) of row r32 in registers 4 g .. 4 g + 3 of half h: one
+// 8-byte read per (h, g), unpacked by bias_elem.
+FA2_DEV u32x2 bias_tile_frag(const char* tile, int r32, int hh, int h, int g) {
+  const int off = h * (32 * 64) + r32 * 64 + (((g ^ (r32 >> 2)) & 3) << 4) + 8 * hh;
+  return *(const u32x2*)(tile + off);
+}
+template <int BIASK>
+FA2_DEV float bias_elem(u32x2 bv, int j) {  // element j (0..3) of a 4-key group
+  const uint32_t wd = bv[j >> 1];
+  if constexpr (BIASK == 17) return __uint_as_float((j & 1) ? (wd & 0xFFFF0000u) : (wd << 16));
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)((j & 1) ? (wd >> 16) : (wd & 0xFFFFu)));
+}
+constexpr int kBiasTile = 32 * 64 * 2;  // bytes of one wave's bias tile
+// host side: a bias the LDS-staged paths take (16-bit, every row 16-byte aligned)
+inline bool bias16_rows(const void* bias, int dtype, const int64_t* stride) {
+  return bias && (dtype == 16 || dtype == 17) && ((uintptr_t)bias & 15) == 0 && stride[0] % 8 == 0 &&
+         stride[1] % 8 == 0 && stride[2] % 8 == 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Cross-half exchange: returns {x of lanes 0-31, x of lanes 32-63} in every lane.
 FA2_DEV float half_max(float x) {

@@ -383,10 +383,16 @@ static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
 template <bool BF16, int DT>
 hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
-  // hot path: software-pipelined kernel (fwd_pipe_kernel.h)
+  // hot path: software-pipelined kernel (fwd_pipe_kernel.h), also with a 16-bit bias whose rows
+  // are 16-byte aligned (its tiles are staged by LDS-DMA)
   if constexpr (DT == 64 || DT == 128) {
-    if (aligned && !bi && !dr && a.k_stride[1] == a.v_stride[1])
-      return c ? launch_fwd_pipe<BF16, DT, true>(a, st) : launch_fwd_pipe<BF16, DT, false>(a, st);
+    const bool bias16 = bias16_rows(a.bias, a.bias_dtype, a.bias_stride);
+    if (aligned && !dr && a.k_stride[1] == a.v_stride[1] && (!bi || bias16)) {
+      if (!bi) return c ? launch_fwd_pipe<BF16, DT, true, 0>(a, st) : launch_fwd_pipe<BF16, DT, false, 0>(a, st);
+      if (a.bias_dtype == FA2_BF16)
+        return c ? launch_fwd_pipe<BF16, DT, true, 17>(a, st) : launch_fwd_pipe<BF16, DT, false, 17>(a, st);
+      return c ? launch_fwd_pipe<BF16, DT, true, 16>(a, st) : launch_fwd_pipe<BF16, DT, false, 16>(a, st);
+    }
   }
 #define FA2_FWD_CASE(C, B, R, A)                                  \
   if (c == C && bi == B && dr == R && aligned == A)               \

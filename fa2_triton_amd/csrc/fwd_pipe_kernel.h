@@ -24,20 +24,20 @@
 
 namespace fa2 {
 
-// NW = 4: two independent workgroups per CU.  NW = 8: one workgroup of 256 rows per CU whose
-// two waves per SIMD (w and w + 4) share every K/V tile (half the LDS-DMA per MFMA); with STAG
-// the second half (waves 4-7, group B) runs half a tile behind the first: in every period between
-// two barriers group A runs [X(i) Y(i)] and group B [Y(i-1) X(i)], so each SIMD pairs one wave's
-// exponential-heavy phase X with the other's MFMA-heavy phase Y (MI355X_MICROARCH.md, "Two waves
-// per SIMD", item 9).  V then needs three buffers (group B still reads V(i-1) in period i);
-// four are kept so that the buffer index is t & 3 (with t % 3 the unrolled loop computed the
-// buffer bases at run time and spilled).
-template <bool BF16, int DT, bool CAUSAL, int NW, bool STAG>
+// NW = 4: two independent workgroups per CU; NW = 8 (one workgroup of 256 rows per CU, the two
+// waves of a SIMD sharing every K/V tile) measured neutral to -1 % and is kept for A/Bs.
+// BIASK = 16 / 17: an additive fp16 / bf16 bias with 16-byte aligned rows.  Each wave stages its
+// own [32 rows x 64 keys] bias tile by LDS-DMA (4 KiB, single buffered, wave-private: no barrier
+// involved): the pieces of tile i+1 go out first in phase X(i), and phase Y(i) waits for them
+// with a counted vmcnt that leaves the period's K/V pieces in flight.  The bias enters the scores
+// in phase Y, x = s scale + b (natural units), z = x log2(e) - m_ref, as the reference adds it
+// before the softmax (/root/reference/src/forward/compute_row_blocks.py:58-66).
+template <bool BF16, int DT, bool CAUSAL, int NW, int BIASK>
 __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(!STAG || NW == 8, "the stagger pairs the two waves of a SIMD");
-  constexpr int NKB = 2, NVB = STAG ? 4 : 2;  // K, V tile buffers
+  constexpr bool BIAS = BIASK != 0;
+  constexpr int NKB = 2, NVB = 2;  // K, V tile buffers
   constexpr int NT = NW * 64;
   constexpr int BM = NW * 32;        // query rows per workgroup
   constexpr int BN = 64;             // keys per tile
@@ -48,7 +48,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   constexpr int EPS = 32 / NQK;      // exponentials per QK^T step
   constexpr int TILE = BN * DT * 2;  // bytes per K (or V) tile
   constexpr int LEAD = 3;            // fragment reads in flight ahead of their MFMA
-  __shared__ __attribute__((aligned(16))) char smem[(NKB + NVB) * TILE];  // K buffers, V buffers
+  constexpr int BTILE = BIAS ? kBiasTile : 0;  // bytes per wave's bias tile ([32 rows][BN keys], 16-bit)
+  __shared__ __attribute__((aligned(16))) char smem[(NKB + NVB) * TILE + NW * BTILE];  // K, V, bias tiles
   static_assert(NQK % 8 == 0 && 32 % NQK == 0, "QK^T steps must carry whole pack pairs");
 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branches
@@ -66,7 +67,11 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   const int nrep = PAIR && nmb - 1 - mbi != mbi ? 2 : 1;
   for (int rep = 0; rep < nrep; ++rep) {
   if (rep > 0) __syncthreads();  // every wave is past the first item's LDS epilogue
-  const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
+  // lane-dependent values from an opaque copy of the thread id per item: nothing per-lane (the
+  // DMA offsets above all) is hoisted out of the item loop and kept live across both items
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
   const int mb = PAIR ? (rep == 0 ? nmb - 1 - mbi : mbi) : (CAUSAL ? (nmb - 1 - mbi) : mbi);
   const int b = bh / p.heads_q, hq = bh - b * p.heads_q;
   const int hkv = hq / (p.heads_q / p.heads_kv);
@@ -76,9 +81,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     Lq = Lk = p.cu_seqlens[b + 1] - cu;
   }
   const int m0 = mb * BM;
-  // 8 waves: the two groups take alternate 32-row blocks, so both see the same causal extent
-  const int grp = NW == 8 ? (w >> 2) : 0;
-  const int qw0 = m0 + 32 * (NW == 8 ? 2 * (w & 3) + grp : w);  // first row of this wave
+  // 8 waves: the waves sharing a SIMD (w, w + 4) take alternate 32-row blocks, so both see the
+  // same causal extent
+  const int qw0 = m0 + 32 * (NW == 8 ? 2 * (w & 3) + (w >> 2) : w);  // first row of this wave
   const int qi = qw0 + r32;     // this lane's query row
   const int D = p.head_dim;
 
@@ -96,14 +101,35 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   const int diag = Lk - Lq;  // key j visible to query i iff j <= i + diag
 
   auto kt = [&](int t) { return smem + (t & 1) * TILE; };                       // buffer of K tile t
-  auto vt = [&](int t) { return smem + (NKB + (t & (NVB - 1))) * TILE; };  // buffer of V tile t
+  auto vt = [&](int t) { return smem + (NKB + (t & 1)) * TILE; };                // buffer of V tile t
+  char* const bw = smem + (NKB + NVB) * TILE + w * BTILE;  // this wave's bias tile
   BufStager<DT, BN, NT> kst;  // K and V share row strides (checked by the launcher): one offset set
   kst.init(tid, p.k_stride[1], D);
   const int mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
+  // this wave's bias tiles: [32 rows from qw0][BN keys], row stride bias_stride[2] (16-byte
+  // aligned rows, checked by the launcher); rows past seqlen_q read as zeros, keys past seqlen_k
+  // are masked
+  using BiasStager = BufStager<BN, 32, 64>;
+  BiasStager bst;
+  const uint16_t* bg = nullptr;
+  int brows = 0;
+  if constexpr (BIAS) {
+    bst.init(lane, p.bias_stride[2], BN);
+    brows = BiasStager::max_rows(p.bias_stride[2]);
+    bg = (const uint16_t*)p.bias + b * p.bias_stride[0] + hq * p.bias_stride[1];
+  }
+  auto bias_issue = [&](int t) {
+    if constexpr (BIAS) {
+      const i32x4 r = BiasStager::tile_rsrc(bg + t * BN, p.bias_stride[2], qw0, p.seqlen_q, brows);
+#pragma unroll
+      for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bw, r, it);
+    }
+  };
   if (ntiles > 0) {
     kst.issue(kt(0), kg, p.k_stride[1], 0, Lk, mrows);
     kst.issue(vt(0), vg, p.v_stride[1], 0, Lk, mrows);
     if (ntiles > 1) kst.issue(kt(1), kg, p.k_stride[1], BN, Lk, mrows);
+    bias_issue(0);
   }
 
   // ---- Q fragments (B operand of S^T = K Q^T) ------------------------------------------------
@@ -116,6 +142,10 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   }
 
   const float sc = p.softmax_scale * kLog2e;
+  // Scores enter the softmax as x = score(s) in units of uz: the raw s in units of scale log2(e)
+  // without a bias; x = s scale + b in natural units (uz = log2(e)) with one.  The exponent
+  // argument is z = x uz - m_ref, the running max is kept in log2 units.
+  const float uz = BIAS ? kLog2e : sc;
   float m_run = kNegInf, l_run = 0.f;
   float m_ref = 0.f;  // the max the stored exponent arguments are relative to (0 while m_run = -inf)
   f32x16 acc[NDT];
@@ -132,8 +162,30 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   float mx = kNegInf;  // their (masked) row max, both lane halves combined, times sc
   u32x4 pf[2][2];      // P of the current tile, packed: B operand of O^T += V^T P^T
 
-  // masked raw scores + row max (register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh)
+  // bias of tile t for this lane (register i of half h: key 32 h + (i & 3) + 8 (i >> 2) + 4 hh of
+  // row qi): group g = i >> 2 of half h is one 8-byte read of the staged tile
+  auto bias_frag = [&](int h, int g) -> u32x2 {  // (of the tile in this wave's buffer)
+    if constexpr (BIAS) return bias_tile_frag(bw, r32, hh, h, g);
+    else return u32x2{0u, 0u};
+  };
+  auto bias_val = [&](u32x2 bv, int j) -> float { return bias_elem<BIASK>(bv, j); };
+  // score(s) with the bias of tile t added (BIAS), in place, then masked (MASK: keys >= rel)
+  auto add_bias = [&](f32x16* v) {
+    if constexpr (BIAS) {
+      const float scale = p.softmax_scale;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const u32x2 bv = bias_frag(h, g);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[h][4 * g + j] = fmaf(v[h][4 * g + j], scale, bias_val(bv, j));
+        }
+    }
+  };
+  // masked scores + row max (register i of half t holds key n0 + 32 t + (i & 3) + 8 (i >> 2) + 4 hh)
   auto mask_max = [&](int n0) {
+    add_bias(s);
     const int rel = lim_lane - n0 - 4 * hh;
     float m = kNegInf;
 #pragma unroll
@@ -144,16 +196,17 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
         s[t][i] = o < rel ? s[t][i] : kNegInf;
         m = fmaxf(m, s[t][i]);
       }
-    mx = half_max(m) * sc;
+    mx = half_max(m) * uz;
   };
   auto plain_max = [&]() {
+    add_bias(s);
     float m0_ = kNegInf, m1_ = kNegInf;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       m0_ = fmaxf(m0_, s[0][i]);
       m1_ = fmaxf(m1_, s[1][i]);
     }
-    mx = half_max(fmaxf(m0_, m1_)) * sc;
+    mx = half_max(fmaxf(m0_, m1_)) * uz;
   };
   auto kfrag = [&](const char* K, int m) { return lds_row_frag<DT, BN>(K, 32 * (m & 1), r32, m >> 1, hh); };
   auto vfrag = [&](const char* V, int m) { return lds_tr_frag<DT, BN>(V, 16 * (m / NDT), 32 * (m % NDT), lane); };
@@ -173,7 +226,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     }
   };
 
-  // Defer-max decision for the tile whose exponent arguments z = s * sc - m_ref sit in z[].
+  // Defer-max decision for the tile whose exponent arguments z = x uz - m_ref sit in z[].
   // Usually the running max stays (m_use == m_ref) and z is final; when some row of the wave
   // outgrew it by more than kDeferMax, O and l are rescaled and z shifted (rare: first tiles).
   auto softmax_begin = [&](f32x16* z) {
@@ -201,7 +254,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[t][i] = fmaf(v[t][i], sc, -m_ref);
+      for (int i = 0; i < 16; ++i) v[t][i] = fmaf(v[t][i], uz, -m_ref);
   };
 
   // exponentials e..e+1 of the flat 32-score list -> P, row-sum partials
@@ -214,15 +267,13 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     pf[t][i >> 3][(i & 7) >> 1] = E::pack2(p0, p1);
   };
 
-  __builtin_amdgcn_s_waitcnt(0);  // Q fragments + K0, V0, K1
+  __builtin_amdgcn_s_waitcnt(0);  // Q fragments + K0, V0, K1 (+ bias 0, 1)
   __syncthreads();
 
-  constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per tile
-  // DMA pieces of a period (K and V, one barrier per tile) ride in the period's first phase:
-  // phase X for group A, phase Y for group B
+  constexpr int kPieces = BufStager<DT, BN, NT>::kIters;  // LDS-DMA ops per thread per K/V tile
+  // DMA pieces of a period (K and V; one barrier per tile) ride in phase X
   constexpr int kPerX = 2 * kPieces;
   constexpr int kEveryX = NQK / kPerX > 0 ? NQK / kPerX : 1;
-  constexpr int kEveryY = NPV / kPerX > 0 ? NPV / kPerX : 1;
 
   // Rows past the end read as zeros (buffer range check); tiles wholly past it land in buffers
   // nobody reads again.
@@ -232,8 +283,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   auto dma_v = [&](int t, int pc) {
     kst.piece(vt(t), BufStager<DT, BN, NT>::tile_rsrc(vg, p.v_stride[1], t * BN, Lk, mrows), pc);
   };
-  // One-barrier schedule, period i: K(i+2) -> the buffer of K(i), V(i+1) -> that of V(i-1)
-  // (V(i-2) with the stagger).
+  // One-barrier schedule, period i: K(i+2) -> the buffer of K(i), V(i+1) -> that of V(i-1).
   auto dma = [&](int i, int pc) {
     if (pc < kPieces) dma_k(i + 2, pc);
     else dma_v(i + 1, pc - kPieces);
@@ -251,9 +301,10 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   // i+1 live for this wave), with the period's DMA pieces when DMA.  One key half after the
   // other (nxt[0]: steps 0..KS-1, nxt[1]: KS..2KS-1) while the exponentials consume cur[0] then
   // cur[1]: 48 score registers live at any step, not 64.
-  auto phase_x = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto dma_c, int period) {
-    constexpr bool QK = decltype(qk_c)::value, DMA = decltype(dma_c)::value;
+  auto phase_x = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c) {
+    constexpr bool QK = decltype(qk_c)::value;
     const char* K1 = kt(i + 1);
+    if constexpr (QK) bias_issue(i + 1);  // (this wave read bias tile i in phase Y(i-1))
     softmax_begin(cur);
     float rs0 = 0.f, rs1 = 0.f;
     u32x4 kf[NQK];
@@ -271,45 +322,65 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
       }
 #pragma unroll
       for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
-      if (DMA && m % kEveryX == 0 && m / kEveryX < kPerX) dma(period, m / kEveryX);
+      if (m % kEveryX == 0 && m / kEveryX < kPerX) dma(i, m / kEveryX);
       __builtin_amdgcn_sched_barrier(0);
     }
     l_run += rs0 + rs1;
   };
   // Phase Y(i): PV(i) with the row max and exponent arguments of S(i+1) in nxt when QK (masked
-  // when MASK), one v_max3 per step; the period's DMA pieces when DMA.
-  auto phase_y = [&](int i, f32x16* nxt, auto qk_c, auto mask_c, auto dma_c, int period) {
-    constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value, DMA = decltype(dma_c)::value;
+  // when MASK; bias of tile i+1 added first), one v_max3 per step.
+  auto phase_y = [&](int i, f32x16* nxt, auto qk_c, auto mask_c) {
+    constexpr bool QK = decltype(qk_c)::value, MASK = decltype(mask_c)::value;
     const char* V0 = vt(i);
     constexpr int L = 2 * LEAD > NPV ? NPV : 2 * LEAD;
     constexpr int PER = 32 / NPV;
     u32x4 vf[NPV];
     float ma = kNegInf, mb_ = kNegInf;
     const int rel = lim_lane - (i + 1) * BN - 4 * hh;
+    // bias of tile i+1, one 4-key group per read: key half 0 read up front, half 1 two steps
+    // before its first element (fewer registers live than all eight reads at once)
+    u32x2 bz[2][4];
+    auto read_bias = [&](int h) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bz[h][g] = bias_frag(h, g);
+    };
+    if constexpr (BIAS && QK) {
+      // bias tile i+1 (issued first in phase X(i)) has landed; the period's K/V pieces after it
+      // may stay in flight
+      if constexpr (kPerX == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (kPerX == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (kPerX == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else vm_wait_all();
+      read_bias(0);
+    }
+    const float scale = p.softmax_scale;
 #pragma unroll
     for (int j = 0; j < L; ++j) vf[j] = vfrag(V0, j);
 #pragma unroll
     for (int m = 0; m < NPV; ++m) {
       if (m + L < NPV) vf[m + L] = vfrag(V0, m + L);
+      if constexpr (BIAS && QK) {
+        if (m == (NPV / 2 >= 2 ? NPV / 2 - 2 : 0)) read_bias(1);
+      }
       const int kk = m / NDT;
       acc[m % NDT] = E::mfma(vf[m], pf[kk >> 1][kk & 1], acc[m % NDT]);
       if constexpr (QK) {
 #pragma unroll
         for (int e = m * PER; e < (m + 1) * PER; ++e) {
           const int t = e >> 4, r = e & 15;
+          if constexpr (BIAS) nxt[t][r] = fmaf(nxt[t][r], scale, bias_val(bz[t][r >> 2], r & 3));
           if constexpr (MASK) {
             const int o = 32 * t + (r & 3) + 8 * (r >> 2);
             nxt[t][r] = o < rel ? nxt[t][r] : kNegInf;
           }
           float& mm = t ? mb_ : ma;
           mm = fmaxf(mm, nxt[t][r]);
-          nxt[t][r] = fmaf(nxt[t][r], sc, -m_ref);
+          nxt[t][r] = fmaf(nxt[t][r], uz, -m_ref);
         }
       }
-      if (DMA && m % kEveryY == 0 && m / kEveryY < kPerX) dma(period, m / kEveryY);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * sc;
+    if constexpr (QK) mx = half_max(fmaxf(ma, mb_)) * uz;
   };
   auto sync = [&]() {
     vm_wait_all();
@@ -317,7 +388,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   };
   auto dma_only = [&](int period) {
 #pragma unroll
-    for (int pc = 0; pc < 2 * kPieces; ++pc) dma(period, pc);
+    for (int pc = 0; pc < kPerX; ++pc) dma(period, pc);
   };
   using T = std::true_type;
   using F = std::false_type;
@@ -333,24 +404,11 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     last = ntiles - 1;
     if (CAUSAL) last = min(last, (qw0 + 31 + diag) / BN);
   }
-  // One period: X(i) then Y(i).  Group A ends the period after Y(i); with the stagger group B
-  // ends it between X(i) and Y(i), so B's Y(i) runs in the next period beside A's X(i+1): every
-  // wave passes the same number of barriers, B half a tile later.
-  const bool late = STAG && grp == 1;
-  // The conditional barrier is one asm statement (the branch around s_barrier is inside it): as
-  // an if() around __syncthreads() it split the period into basic blocks and the compiler spilled.
-  const uint32_t late_s = __builtin_amdgcn_readfirstlane(late ? 1u : 0u);
-  auto bar_if = [&](uint32_t flag) {
-    asm volatile(
-        "s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_barrier\n1:"
-        :: "s"(flag) : "memory", "scc");
-  };
+  // one period: X(i), Y(i), barrier
   auto step = [&](int i, f32x16* cur, f32x16* nxt, auto qk_c, auto mask_c) {
-    phase_x(i, cur, nxt, qk_c, T{}, i);
-    if constexpr (STAG) bar_if(late_s);
-    phase_y(i, nxt, qk_c, mask_c, F{}, i);
-    if constexpr (STAG) bar_if(late_s ^ 1u);
-    else sync();
+    phase_x(i, cur, nxt, qk_c);
+    phase_y(i, nxt, qk_c, mask_c);
+    sync();
   };
   // steady periods (tile i+1 live and unmasked) unrolled by two with the roles of the two score
   // arrays swapped, so no register copies between periods
@@ -382,7 +440,6 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
     dma_only(i);
     sync();
   }
-  if (STAG) __syncthreads();  // group B's last phase Y reads a V buffer the epilogue reuses
   vm_wait_all();
 
   // ---- epilogue ----------------------------------------------------------------------------
@@ -402,21 +459,13 @@ __global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args
   }
 }
 
-#ifndef FA2_FWD_NW
-#define FA2_FWD_NW 4
-#endif
-#ifndef FA2_FWD_STAG
-#define FA2_FWD_STAG 0
-#endif
-
-template <bool BF16, int DT, bool CAUSAL>
+template <bool BF16, int DT, bool CAUSAL, int BIASK>
 static hipError_t launch_fwd_pipe(const fa2_fwd_args& a, hipStream_t st) {
-  constexpr int NW = FA2_FWD_NW;
-  constexpr bool STAG = NW == 8 && FA2_FWD_STAG;
+  constexpr int NW = 4;
   constexpr int BM = NW * 32;
   const int nmb = (a.seqlen_q + BM - 1) / BM;
   dim3 grid((CAUSAL ? (nmb + 1) / 2 : nmb) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, NW, STAG>), grid, dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((fwd_pipe_kernel<BF16, DT, CAUSAL, NW, BIASK>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
 

@@ -94,9 +94,9 @@ def kernels():
 # hot instantiations: bf16 / fp16 (Lb1 / Lb0), D tiles 64 and 128, causal and not; the plain
 # path (no bias, no dropout, aligned; dQ in the input dtype)
 HOT = {
-    "fwd_pipe": r"_ZN3fa215fwd_pipe_kernelILb[01]ELi(64|128)ELb[01]ELi[48]ELb[01]EEEv12fa2_fwd_args",
-    "dq": r"_ZN3fa29dq_kernelILb[01]ELi(64|128)ELb[01]ELb0ELb0ELb1ELb0EEEv12fa2_bwd_args",
-    "dkdv": r"_ZN3fa211dkdv_kernelILb[01]ELi(64|128)ELb[01]ELb0ELb0ELb1EEEv12fa2_bwd_argsi",
+    "fwd_pipe": r"_ZN3fa215fwd_pipe_kernelILb[01]ELi(64|128)ELb[01]ELi4ELi0EEEv12fa2_fwd_args",
+    "dq": r"_ZN3fa29dq_kernelILb[01]ELi(64|128)ELb[01]ELi0ELb0ELb1ELb0EEEv12fa2_bwd_args",
+    "dkdv": r"_ZN3fa211dkdv_kernelILb[01]ELi(64|128)ELb[01]ELi0ELb0ELb1EEEv12fa2_bwd_argsi",
 }
 
 

@@ -56,6 +56,39 @@ def test_bias_shapes_gqa(dtype, causal, shape, bias_dtype, d):
     torch.testing.assert_close(lse[:, :, :sq][fin], ref_lse[fin], rtol=1e-3, atol=1e-3)
 
 
+PIPE_BIAS_CASES = [
+    # b, hq, hkv, sq, sk, d: key counts multiples of 8, so the bias rows are 16-byte aligned and
+    # the forward runs the pipelined kernel with LDS-staged bias tiles (fwd_pipe_kernel BIASK)
+    (2, 4, 2, 512, 512, 128),
+    (1, 3, 3, 384, 640, 64),
+    (2, 2, 1, 1000, 1000, 80),
+    (1, 2, 2, 129, 256, 128),
+    (1, 2, 2, 700, 136, 64),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PIPE_BIAS_CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", ["b_hq", "1_1", "1_hq"])
+@pytest.mark.parametrize("bias_dtype", ["same", "other16"])
+def test_bias_pipelined_forward(case, dtype, causal, shape, bias_dtype):
+    """The 16-bit, 16-byte-aligned bias path of the pipelined forward (bf16 and fp16 bias in
+    either input dtype), O / dQ / dK / dV under the reference rule and LSE2 against the oracle."""
+    b, hq, hkv, sq, sk, d = case
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, d, dtype)
+    bb, bh = {"b_hq": (b, hq), "1_hq": (1, hq), "1_1": (1, 1)}[shape]
+    bdt = dtype if bias_dtype == "same" else ({torch.bfloat16: torch.float16, torch.float16: torch.bfloat16}[dtype])
+    bias = (torch.rand(bb, bh, sq, sk, device=q.device) * 4 - 2).to(bdt)
+    _check(q, k, v, do, causal, bias, grads_of=(q, k, v))
+    with torch.no_grad():
+        _, lse, _, _ = _flash_attn_forward(q, k, v, None, bias, 0.0, causal, None, None)
+    ref_lse = lse2_reference(q, k, attn_bias=bias, causal=causal)
+    fin = torch.isfinite(ref_lse)
+    torch.testing.assert_close(lse[:, :, :sq][fin], ref_lse[fin], rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("d", [64, 96, 128])
