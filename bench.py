@@ -343,7 +343,9 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
-    device = torch.device("cpu") if args.dry_run else torch.device("cuda", local_rank)
+    # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal of the multi-rank path on
+    # one card) the ranks share them round-robin -- device_count() does not initialise the GPU
+    device = torch.device("cpu") if args.dry_run else torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
 
     global_batch, (lo, hi), scaling = plan(args, world, rank)
     b, h, hkv, s, d = hi - lo, args.heads, args.heads_kv, args.seqlen, args.head_dim
