@@ -488,21 +488,32 @@ FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool vali
   }
 }
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the backend emits two v_xor_b32 here.
+// c must be wave-uniform (it is bound to an SGPR).
+FA2_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Philox4x32-10, first output word, counter (lo, hi, 0, 0), key (seed_lo, seed_hi), converted
 // to [0,1) exactly like Triton's tl.rand (triton/language/random.py:13-156; see
 // oracle/philox.py).  Used for the forward dropout mask keep = rand > p
-// (/root/reference/src/forward/compute_row_blocks.py:76-79).
+// (/root/reference/src/forward/compute_row_blocks.py:76-79).  seed is a kernel argument (wave-uniform:
+// the round keys live in SGPRs).
 FA2_DEV float philox_uniform(uint64_t seed, uint64_t offset) {
   uint32_t c0 = (uint32_t)offset, c1 = (uint32_t)(offset >> 32), c2 = 0, c3 = 0;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t a0 = c0, a2 = c2;
-    c0 = __umulhi(0xCD9E8D57u, a2) ^ c1 ^ k0;
-    c2 = __umulhi(0xD2511F53u, a0) ^ c3 ^ k1;
-    c1 = 0xCD9E8D57u * a2;
-    c3 = 0xD2511F53u * a0;
+    // one 32 x 32 -> 64-bit product per multiplier (v_mad_u64_u32) gives both the high word
+    // and the low word: half the integer multiplies of separate mul_hi / mul_lo
+    const uint64_t pa = (uint64_t)0xCD9E8D57u * c2, pb = (uint64_t)0xD2511F53u * c0;
+    c0 = xor3((uint32_t)(pa >> 32), c1, k0);
+    c2 = xor3((uint32_t)(pb >> 32), c3, k1);
+    c1 = (uint32_t)pa;
+    c3 = (uint32_t)pb;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
