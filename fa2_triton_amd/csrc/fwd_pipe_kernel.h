@@ -32,8 +32,13 @@ namespace fa2 {
 // with a counted vmcnt that leaves the period's K/V pieces in flight.  The bias enters the scores
 // in phase Y, x = s scale + b (natural units), z = x log2(e) - m_ref, as the reference adds it
 // before the softmax (/root/reference/src/forward/compute_row_blocks.py:58-66).
+// Occupancy: two workgroups per CU (<= 256 VGPRs); three for the non-causal D <= 64 forward
+// without bias (<= 168 VGPRs, 96 KiB of LDS), where the softmax VALU per MFMA doubles and the
+// third wave per SIMD pays: a 176-VGPR build (two waves) ran cfg2 10 % slower (profiles/
+// r03_ab_fwd_handoff.txt).  The causal D = 64 kernel spills at 168 and keeps two.
 template <bool BF16, int DT, bool CAUSAL, int NW, int BIASK>
-__global__ void __launch_bounds__(NW * 64, 2) fwd_pipe_kernel(const fa2_fwd_args p) {
+__global__ void __launch_bounds__(NW * 64, DT <= 64 && !CAUSAL && NW == 4 && BIASK == 0 ? 3 : 2)
+    fwd_pipe_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr bool BIAS = BIASK != 0;

@@ -1,6 +1,7 @@
 """A/B timing of several libfa2_amd.so builds in ONE process (interleaved rounds), cfg3 causal.
 
-usage: python scripts/ab.py lib_a.so lib_b.so [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd, SHAPE=B,H,S,D)
+usage: python scripts/ab.py lib_a.so lib_b.so[:ENV=VAL,...] [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd,
+       SHAPE=B,H,S,D; a ":ENV=VAL" suffix sets those variables while that arm runs)
 WHAT: fwd | dkdv, dq (backward stages) | bwd (whole backward)
 """
 import ctypes
@@ -16,14 +17,18 @@ from fa2_triton_amd.backward import _flash_attn_backward  # noqa: E402
 from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
 
 libs = []
-for path in sys.argv[1:]:
+envs = {}
+for arg in sys.argv[1:]:
+    path, _, env = arg.partition(":")
     lib = ctypes.CDLL(os.path.abspath(path))
     lib.fa2_fwd.argtypes = [ctypes.POINTER(L.FwdArgs), ctypes.c_void_p]
     lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(L.BwdArgs), ctypes.c_int, ctypes.c_void_p]
     lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.c_void_p, ctypes.c_void_p]
     lib.fa2_last_error.restype = ctypes.c_char_p
-    libs.append((os.path.basename(path), lib))
+    name = os.path.basename(path) + (":" + env if env else "")
+    envs[name] = dict(kv.split("=", 1) for kv in env.split(",")) if env else {}
+    libs.append((name, lib))
 
 b, h, s, d = (int(x) for x in os.environ.get("SHAPE", "8,32,4096,128").split(","))  # B, H, S, D
 causal = os.environ.get("CAUSAL", "1") == "1"
@@ -39,6 +44,10 @@ results = {(n, w): [] for n, _ in libs for w in what}
 for rnd in range(5):
     for name, lib in libs:
         L._lib = lib
+        for kv in envs.values():
+            for k_ in kv:
+                os.environ.pop(k_, None)
+        os.environ.update(envs[name])
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
         delta = torch.empty_like(lse)
         _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=1, _delta=delta)

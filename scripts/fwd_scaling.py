@@ -1,4 +1,5 @@
 """Forward time vs sequence length (fixed B*H), to separate per-tile from per-workgroup costs."""
+import argparse
 import os
 import sys
 
@@ -7,10 +8,17 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
 
-b, h, d = 8, 32, 128
-for causal in (False, True):
-    for s in (1024, 2048, 4096, 8192):
-        bb = max(1, b * 4096 // s)  # keep B*S constant: same number of query blocks
+ap = argparse.ArgumentParser()
+ap.add_argument("--d", type=int, default=128)
+ap.add_argument("--heads", type=int, default=32)
+ap.add_argument("--tokens", type=int, default=32768, help="B*S, constant over the sweep")
+ap.add_argument("--seqlens", default="1024,2048,4096,8192")
+ap.add_argument("--causal", default="0,1")
+args = ap.parse_args()
+h, d = args.heads, args.d
+for causal in [bool(int(c)) for c in args.causal.split(",")]:
+    for s in [int(x) for x in args.seqlens.split(",")]:
+        bb = max(1, args.tokens // s)  # keep B*S constant: same number of query blocks
         q = torch.empty(bb, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
         k = torch.empty_like(q).normal_(0, 0.5)
         v = torch.empty_like(q).normal_(0, 0.5)
