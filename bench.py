@@ -263,7 +263,8 @@ def load_pmc():
     symbol, file name)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    # by name: the round tags (r01.., r02a.., r03a..) order them; file times do not survive a checkout
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
         return {}, None
     data = json.load(open(files[-1]))
