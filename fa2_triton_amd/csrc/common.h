@@ -522,4 +522,19 @@ FA2_DEV float philox_uniform(uint64_t seed, uint64_t offset) {
   return (float)x * 4.6566127342e-10f;
 }
 
+// Dropout keep bits of one lane's 16 accumulator registers: bit i = (philox_uniform(seed,
+// base + o(i) * step) > p), o(i) = (i & 3) + 8 (i >> 2) (the register's row or key offset in a
+// 32 x 32 accumulator).  A rolled loop (two chains in flight) for dkdv_kernel's step start: fully
+// unrolled next to its MFMA operands, the 16 Philox states spilled 180-230 bytes per lane
+// (cfg3 dropout dK/dV 6.51 -> 5.42 ms with this, r03k).
+FA2_DEV uint32_t dropout_keep16(uint64_t seed, uint64_t base, uint64_t step, float p) {
+  uint32_t bits = 0;
+#pragma unroll 2
+  for (int i = 0; i < 16; ++i) {
+    const uint64_t o = (uint64_t)((i & 3) + 8 * (i >> 2));
+    bits |= (philox_uniform(seed, base + o * step) > p ? 1u : 0u) << i;
+  }
+  return bits;
+}
+
 }  // namespace fa2

@@ -120,3 +120,33 @@ def test_cfg4_batch_shard(rank):
         assert torch.isfinite(t).all()
     for b, h in ((0, 5), (7, 30)):
         _slice_check(q, k, v, do, out, grads, lse, b, h, 1, True, tag=f"cfg4 rank{rank} (global row {lo + b})")
+
+
+@pytest.mark.gpu
+def test_cfg4_every_shard_equals_the_full_batch():
+    """configs[3] on all 8 ranks: each rank's shard (bench.shard_batch), run as its own B=8
+    launch, gives bit for bit the rows of one B=64 launch of the whole batch -- O, LSE, dQ, dK,
+    dV of every (batch, head), no sampling.  Batch rows are independent and every kernel is
+    deterministic whatever workgroup computes a row block, so the 8-GPU job equals the 1-GPU
+    B=64 run exactly; the oracle checks of the sampled shards above then cover all 8."""
+    import bench
+    from fa2_triton_amd import flash_attn_func
+    from fa2_triton_amd.forward import _flash_attn_forward
+
+    qa, ka, va, doa = generate_test_data(64, 32, 32, 4096, 4096, 128, torch.bfloat16)
+    with torch.no_grad():
+        _, lse_full, _, _ = _flash_attn_forward(qa, ka, va, None, None, 0.0, True, None, None)
+    out_full = flash_attn_func(qa, ka, va, None, None, 0.0, True)
+    g_full = torch.autograd.grad(out_full, (qa, ka, va), doa)
+    out_full = out_full.detach()
+    for rank in range(8):
+        lo, hi = bench.shard_batch(64, 8, rank)
+        q, k, v = (t.detach()[lo:hi].clone().requires_grad_() for t in (qa, ka, va))
+        with torch.no_grad():
+            _, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, True, None, None)
+        out = flash_attn_func(q, k, v, None, None, 0.0, True)
+        grads = torch.autograd.grad(out, (q, k, v), doa[lo:hi])
+        assert torch.equal(out.detach(), out_full[lo:hi]), rank
+        assert torch.equal(lse, lse_full[lo:hi]), rank
+        for name, g, gf in zip(("dq", "dk", "dv"), grads, g_full):
+            assert torch.equal(g, gf[lo:hi]), (rank, name)
