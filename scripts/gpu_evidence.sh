@@ -1,7 +1,9 @@
 #!/bin/bash
-# One GPU call of round evidence: full parity suite, smoke(), a bench line per BASELINE config
-# (cfg3 default, cfg2, cfg5) and the bias / dropout legs of cfg3, each step under its own limit.
-# usage: bash scripts/gpu_evidence.sh TAG
+# One GPU call of round evidence: full parity suite (rtol log), smoke(), a bench line per BASELINE
+# config (cfg3 default, cfg2, cfg5), the bias / dropout / non-causal legs of cfg3, a two-rank
+# rehearsal of the multi-GPU launcher on this one GPU, then scripts/profile_round.sh (rocprofv3
+# kernel stats + PMC passes), each step under its own limit.
+# usage: bash scripts/gpu_evidence.sh TAG    then   python scripts/summarize_profiles.py TAG
 set -o pipefail
 TAG=${1:-run}
 OUT=gpurun_out/$TAG
@@ -22,4 +24,10 @@ cat $OUT/bench_cfg5.json
 timeout -k 10 300 python bench.py --bias --no-cpu-baseline > $OUT/bench_cfg3_bias.json 2> $OUT/bench_bias.err || exit $?
 timeout -k 10 300 python bench.py --dropout 0.1 --no-cpu-baseline > $OUT/bench_cfg3_dropout.json 2> $OUT/bench_dropout.err || exit $?
 timeout -k 10 300 python bench.py --no-causal --no-cpu-baseline > $OUT/bench_cfg3_noncausal.json 2> $OUT/bench_nc.err || exit $?
-for f in bias dropout noncausal; do python -c "import json,sys; d=json.load(open('$OUT/bench_cfg3_$f.json')); print('$f', d['value'], d['fwd_tflops'], d['bwd_tflops'], d['kernels'])"; done
+timeout -k 10 300 python bench.py --bias --no-causal --no-cpu-baseline > $OUT/bench_cfg3_bias_noncausal.json 2> $OUT/bench_bias_nc.err || exit $?
+for f in bias dropout noncausal bias_noncausal; do python -c "import json,sys; d=json.load(open('$OUT/bench_cfg3_$f.json')); print('$f', d['value'], d['fwd_tflops'], d['bwd_tflops'], d['kernels'])"; done
+# two ranks on the one GPU of this box: the self-launching multi-GPU path end to end (gloo
+# coordination, per-rank shards, max-over-ranks timing); the 8-GPU run is the driver's
+timeout -k 10 400 python bench.py --gpus 2 --steps 10 --no-cpu-baseline > $OUT/bench_cfg3_2ranks.json 2> $OUT/bench_2ranks.err || exit $?
+cat $OUT/bench_cfg3_2ranks.json
+bash scripts/profile_round.sh $TAG
