@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   __shared__ __attribute__((aligned(16))) char smem[VT + 4 * QT + 2 * ST + (BIASL ? 4 * kBiasKTile : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the same, in an SGPR: scalar branches
   const int r32 = lane & 31, hh = lane >> 5;
   const int nkb = (p.seqlen_k + BNK - 1) / BNK;
   const int item = xcd_item(blockIdx.x, gridDim.x);  // head-major, see xcd_item
@@ -174,16 +175,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       stage_tile<DT, BMQ, NT, false>(qt(buf), qg, p.q_stride[1], m, Lq, D, tid);
       stage_tile<DT, BMQ, NT, false>(ot(buf), og, p.do_stride[1], m, Lq, D, tid);
     }
-    if (w == 0) {  // LSE2 rows -> lanes 0..31, delta rows -> lanes 32..63 (one 256-byte piece)
+    if (wu < 2) {  // LSE2 rows (wave 0) then delta rows (wave 1): 32 dwords each, lanes 0..31
       // wave-uniform row bases in SGPR descriptors (no per-lane 64-bit address at the register
-      // limit); each half-wave issues the piece of its own array
+      // limit)
       const int64_t row0 = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride + m;
-      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf)));
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf))) + wu * BMQ * 4;
       int t = threadIdx.x;
       asm volatile("" : "+v"(t));
-      const uint32_t voff = (uint32_t)(t & 31) * 4u;
-      if (((t >> 5) & 1) == 0) blds4(voff, make_rsrc(p.lse + row0, BMQ * 4), lds);
-      else blds4(voff, make_rsrc(p.delta + row0, BMQ * 4), lds);
+      blds4_lo32((uint32_t)(t & 31) * 4u, make_rsrc((wu == 0 ? p.lse : p.delta) + row0, BMQ * 4), lds);
     }
   };
   // The same staging for the descending sweep with every address carried from step to step in
@@ -213,13 +212,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
       qst.piece(qt(buf), rq, it);
       ost.piece(ot(buf), ro, it);
     }
-    if (w == 0) {
-      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf)));
+    if (wu < 2) {
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(st(buf))) + wu * BMQ * 4;
       int t = threadIdx.x;
       asm volatile("" : "+v"(t));
-      const uint32_t voff = (uint32_t)(t & 31) * 4u;
-      if (((t >> 5) & 1) == 0) blds4(voff, make_rsrc(p.lse + nl, BMQ * 4), lds);
-      else blds4(voff, make_rsrc(p.delta + nl, BMQ * 4), lds);
+      blds4_lo32((uint32_t)(t & 31) * 4u, make_rsrc((wu == 0 ? p.lse : p.delta) + nl, BMQ * 4), lds);
     }
     if (++st_mt == n_mt) {
       st_mt = 0;

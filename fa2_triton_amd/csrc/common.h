@@ -369,6 +369,19 @@ FA2_DEV void blds4(uint32_t voff, i32x4 rsrc, uint32_t lds_base_uniform) {
       : "memory");
 }
 
+// The same for lanes 0..31 only (EXEC's high half cleared around the one instruction and
+// restored): a 32-dword row piece from a whole-wave branch, without a divergent branch per half.
+FA2_DEV void blds4_lo32(uint32_t voff, i32x4 rsrc, uint32_t lds_base_uniform) {
+  uint32_t keep;
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\ts_mov_b32 exec_hi, 0\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 1\n\t"
+      "buffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+      : "=&s"(keep), "=&s"(save)
+      : "v"(voff), "s"(rsrc), "s"(lds_base_uniform)
+      : "memory");
+}
+
 template <int DT, int ROWS, int NTHREADS>
 struct BufStager {
   static constexpr int kPieces = ROWS * DT / 8;
