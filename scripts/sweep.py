@@ -4,7 +4,7 @@ S) with 32 heads, bf16, inputs resident in HBM; fwd and fwd+bwd through flash_at
 of HIP-event-timed calls; TFLOP/s use the algorithmic count (fwd 4 B H S^2 D, x0.5 causal;
 bwd 2.5x fwd).
 
-usage: python scripts/sweep.py [--reps 10]   (one JSON line per point)
+usage: python scripts/sweep.py [--reps 10] [--dims 64,128] [--seqlens 1024,...]   (one JSON line per point)
 """
 import argparse
 import json
@@ -37,10 +37,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=32768)
+    ap.add_argument("--dims", default="64,128", help="head dims")
+    ap.add_argument("--seqlens", default="1024,2048,4096,8192,16384")
     args = ap.parse_args()
     h = 32
-    for d in (64, 128):
-        for s in (1024, 2048, 4096, 8192, 16384):
+    for d in [int(x) for x in args.dims.split(",")]:
+        for s in [int(x) for x in args.seqlens.split(",")]:
             b = max(1, args.tokens // s)
             for causal in (False, True):
                 torch.manual_seed(0)
