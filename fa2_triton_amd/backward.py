@@ -19,7 +19,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, stream_of
+from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, launch_on
 
 
 def _fill_args(args, q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, causal: bool) -> None:
@@ -129,8 +129,7 @@ def _flash_attn_backward(
         args.dkv_workspace, args.dkv_workspace_bytes = dkv_ws.data_ptr(), dkv_ws.numel()
     stages = _stages if _stages is not None else (14 if bias_grad else 6)
     lib = _lib.load()
-    with torch.cuda.device(q.device):
-        _lib.check(lib.fa2_bwd_stages(ctypes.byref(args), stages, stream_of(q)))
+    _lib.check(launch_on(q, lambda st: lib.fa2_bwd_stages(ctypes.byref(args), stages, st)))
     if not bias_grad:
         return dq, dk, dv
     return dq, dk, dv, dbias32.view(bias.shape).to(bias.dtype)

@@ -14,7 +14,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, stream_of
+from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, launch_on
 
 
 def _flash_attn_forward(
@@ -72,6 +72,5 @@ def _flash_attn_forward(
     args.dropout_p = float(dropout_p)
     args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
     lib = _lib.load()
-    with torch.cuda.device(q.device):
-        _lib.check(lib.fa2_fwd(ctypes.byref(args), stream_of(q)))
+    _lib.check(launch_on(q, lambda st: lib.fa2_fwd(ctypes.byref(args), st)))
     return o, lse, softmax_scale, dropout_seed

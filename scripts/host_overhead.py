@@ -31,8 +31,8 @@ res = {
     "_flash_attn_forward": per_call(lambda: _flash_attn_forward(q, k, v, None, None, 0.0, False, None, None)),
     "flash_attn_func (no grad)": per_call(lambda: flash_attn_func(q, k, v)),
     "torch.empty x2": per_call(lambda: (torch.empty_like(q), torch.empty((1, 1, 128), device=q.device, dtype=torch.float32))),
-    "stream_of": per_call(lambda: stream_of(q)),
-    "raw stream": per_call(lambda: torch._C._cuda_getCurrentRawStream(q.device.index)),
+    "current_stream().cuda_stream": per_call(lambda: torch.cuda.current_stream(q.device).cuda_stream),
+    "stream_of (raw)": per_call(lambda: stream_of(q)),
     "torch.cuda.device ctx": per_call(lambda: torch.cuda.device(q.device).__enter__()),
     "FwdArgs()": per_call(lambda: _lib.FwdArgs()),
 }
