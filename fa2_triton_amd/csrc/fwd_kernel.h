@@ -24,6 +24,8 @@
 #include "common.h"
 #include "fa2_internal.h"
 #include "fwd_pipe_kernel.h"
+#include "fwd_w64_kernel.h"
+#include <stdlib.h>
 
 namespace fa2 {
 
@@ -388,6 +390,10 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   if constexpr (DT == 64 || DT == 128) {
     const bool bias16 = bias16_rows(a.bias, a.bias_dtype, a.bias_stride);
     if (aligned && !dr && a.k_stride[1] == a.v_stride[1] && (!bi || bias16)) {
+      if constexpr (DT == 128) {
+        static const bool w64 = getenv("FA2_FWD_W64") && atoi(getenv("FA2_FWD_W64")) != 0;
+        if (!bi && w64) return c ? launch_fwd_w64<BF16, DT, true>(a, st) : launch_fwd_w64<BF16, DT, false>(a, st);
+      }
       if (!bi) return c ? launch_fwd_pipe<BF16, DT, true, 0>(a, st) : launch_fwd_pipe<BF16, DT, false, 0>(a, st);
       if (a.bias_dtype == FA2_BF16)
         return c ? launch_fwd_pipe<BF16, DT, true, 17>(a, st) : launch_fwd_pipe<BF16, DT, false, 17>(a, st);
