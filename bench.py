@@ -377,6 +377,7 @@ def main():
     torch.cuda.set_device(device)
     from fa2_triton_amd import flash_attn_func
     from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.utils import dropout_mask_words
     from fa2_triton_amd.forward import _flash_attn_forward
 
     dtype = DTYPES[args.dtype]
@@ -421,14 +422,19 @@ def main():
     reps = max(5, args.steps)
     stream = torch.cuda.current_stream(device)
     with torch.no_grad():
-        o, lse, _, _ = _flash_attn_forward(q, k, v, None, bias, p_drop, causal, None, seed)
+        # with dropout, as in the autograd op: the forward saves its keep bits, the backward reads them
+        kmask = None
+        if p_drop > 0:
+            kmask = torch.empty(dropout_mask_words(b, h, s, s), dtype=torch.int32, device=device)
+        o, lse, _, _ = _flash_attn_forward(q, k, v, None, bias, p_drop, causal, None, seed, dropout_mask=kmask)
         delta = torch.empty_like(lse)  # shared by the stage calls: written by dQ, read by dK/dV
 
         def bwd(stages):
             return lambda: _flash_attn_backward(do, q, k, v, bias, None, o, lse, p_drop, causal, None, seed,
-                                                _stages=stages, _delta=delta)
+                                                _stages=stages, _delta=delta, dropout_mask=kmask)
 
-        calls = {"fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, bias, p_drop, causal, None, seed)}
+        calls = {"fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, bias, p_drop, causal, None, seed,
+                                                           dropout_mask=kmask)}
         if not fwd_only:
             calls.update(dq_kernel=bwd(4), dkdv_kernel=bwd(2))
         times = {}

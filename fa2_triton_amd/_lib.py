@@ -52,6 +52,7 @@ class FwdArgs(ctypes.Structure):
         ("softmax_scale", ctypes.c_float),
         ("dropout_p", ctypes.c_float),
         ("dropout_seed", ctypes.c_uint64),
+        ("dropout_mask", ctypes.c_void_p),
     ]
 
 
@@ -98,12 +99,13 @@ class BwdArgs(ctypes.Structure):
         ("dbias_stride", _i64x3),
         ("dkv_workspace", ctypes.c_void_p),
         ("dkv_workspace_bytes", ctypes.c_int64),
+        ("dropout_mask", ctypes.c_void_p),
     ]
 
 
-ABI_VERSION = 5  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 6  # FA2_ABI_VERSION in include/fa2_amd.h
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes",
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes", "fa2_dropout_mask_bytes",
                     "fa2_cu_seqlens_from_mask",
                     "fa2_last_error", "fa2_version")
 
@@ -138,6 +140,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int
         lib.fa2_last_error.argtypes = []
         lib.fa2_last_error.restype = ctypes.c_char_p
+        lib.fa2_dropout_mask_bytes.argtypes = [ctypes.c_int32] * 4
+        lib.fa2_dropout_mask_bytes.restype = ctypes.c_int64
         lib.fa2_version.argtypes = []
         lib.fa2_version.restype = ctypes.c_int
         version = lib.fa2_version()

@@ -19,7 +19,8 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, launch_on
+from .utils import (bshd_strides, check_dropout_mask, cu_seqlens_from_mask, encode_dtype, handle_dropout,
+                    infer_bias_strides, launch_on)
 
 
 def _fill_args(args, q: Tensor, k: Tensor, v: Tensor, o: Tensor, dO: Tensor, causal: bool) -> None:
@@ -68,6 +69,7 @@ def _flash_attn_backward(
     _stages: Optional[int] = None,
     _delta: Optional[Tensor] = None,
     bias_grad: bool = False,
+    dropout_mask: Optional[Tensor] = None,
 ):
     """Returns (dq, dk, dv) -- the reference's contract -- or (dq, dk, dv, dbias) with
     `bias_grad=True`: dbias = dL/d(bias) in bias's shape and dtype.  The library's bias-gradient
@@ -124,6 +126,9 @@ def _flash_attn_backward(
     args.softmax_scale = float(softmax_scale)
     args.dropout_p = float(dropout_p)
     args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
+    if dropout_mask is not None and dropout_p > 0.0:  # the forward's keep bits, read instead of redrawn
+        check_dropout_mask(dropout_mask, batch, nheads_q, seqlen_q, seqlen_k, q.device)
+        args.dropout_mask = dropout_mask.data_ptr()
     dkv_ws = alloc_dkv_workspace(args, q.device)
     if dkv_ws is not None:
         args.dkv_workspace, args.dkv_workspace_bytes = dkv_ws.data_ptr(), dkv_ws.numel()

@@ -157,6 +157,11 @@ int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* a) {
   return fa2::dkv_workspace_bytes(a->batch, a->heads_q, a->heads_kv, a->seqlen_k, a->head_dim);
 }
 
+int64_t fa2_dropout_mask_bytes(int32_t batch, int32_t heads_q, int32_t seqlen_q, int32_t seqlen_k) {
+  if (batch < 1 || heads_q < 1 || seqlen_q < 1 || seqlen_k < 1) return 0;
+  return (int64_t)batch * heads_q * ((seqlen_q + 31) / 32) * ((seqlen_k + 31) / 32) * 128;
+}
+
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,
                              int32_t* cu_seqlens, void* stream) {
   if (!mask || !cu_seqlens || batch < 1 || seqlen < 0) return fail(FA2_E_INVALID, "bad cu_seqlens arguments");

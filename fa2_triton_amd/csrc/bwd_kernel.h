@@ -276,15 +276,40 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   for (int dt = 0; dt < NDT; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
 
 
+  // dropout keep words (the forward's saved mask, tiled layout of fa2_amd.h) of a step: lane
+  // (r32, hh) loads row r32 of the step's 32 x 32 tile; loaded one step ahead so the loop's
+  // vm_wait_all retires them (a load consumed in its own step would wait for the Q / dO DMA)
+  uint32_t mw_cur = 0u, mw_nxt = 0u;
+  auto load_mw = [&](int hq_, int m_) -> uint32_t {
+    if constexpr (DROPOUT && DT <= 128) {
+      if (p.dropout_mask && kw0 < p.seqlen_k) {
+        const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+        return p.dropout_mask[(((int64_t)(b * p.heads_q + hq_) * nrb + (m_ >> 5)) * ncw + (kw0 >> 5)) * 32 + r32];
+      }
+    }
+    return 0u;
+  };
   // Phases (sched_barrier-separated so each phase's LDS fragments stay inside it and the
   // register peak stays under 256): S, dP -> P, dS -> dV, dK.
   auto body = [&](auto mask_c, const char* Q, const char* O, const char* S, int hq, int m, auto next_bias) {
     constexpr bool MASK = decltype(mask_c)::value;
     // the forward's keep mask M of this lane's key and the 16 rows m + o + 4 hh, first: no score
     // or fragment registers are live yet
-    const uint32_t keep16 = DROPOUT ? dropout_keep16(p.dropout_seed, drop_base(hq) + (uint64_t)(m + 4 * hh) * (uint64_t)Lk + (uint64_t)kj,
-                                                     (uint64_t)Lk, p.dropout_p)
-                                    : 0u;
+    uint32_t keep16 = 0u;
+    if constexpr (DROPOUT) {
+      // (D = 256: redrawn -- the mask read there crashes ROCm 7.2's AGPR-copy rewrite pass)
+      if (DT <= 128 && p.dropout_mask) {
+        // the forward's saved 32 x 32 bit tile of this step (rows m.., keys kw0..), loaded one
+        // step ahead: lane (r32, hh) holds row r32's word (bit k = key kw0 + k).  Transposed
+        // across each 32-lane half (5 ds_swizzle xor stages), lane r32 then holds key kw0 + r32's
+        // column (bit r = row m + r); register i of the lane is row (i & 3) + 8 (i >> 2) + 4 hh.
+        const uint32_t xs = transpose32_lanes(mw_cur, r32) >> (4 * hh);
+        keep16 = (xs & 0xFu) | ((xs >> 4) & 0xF0u) | ((xs >> 8) & 0xF00u) | ((xs >> 12) & 0xF000u);
+      } else {
+        keep16 = dropout_keep16(p.dropout_seed, drop_base(hq) + (uint64_t)(m + 4 * hh) * (uint64_t)Lk + (uint64_t)kj,
+                                (uint64_t)Lk, p.dropout_p);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     f32x16 s = zero16(), dp = zero16();
     u32x4 bt2[2];
@@ -541,9 +566,14 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     __syncthreads();
   }
 
+  if (total > 0) mw_cur = load_mw(h0, tile_row(0));
   int g = 0, mt = 0;  // (q-head in group, query tile) of the current step
   for (int step = 0; step < total; ++step) {
     const int cur = step & 1;
+    if (DROPOUT && step + 1 < total) {
+      const bool wrap = mt + 1 == n_mt;
+      mw_nxt = load_mw(h0 + g + (wrap ? 1 : 0), tile_row(wrap ? 0 : mt + 1));
+    }
     if (step + 1 < total) {
       if constexpr (ALIGNED) stage_desc(cur ^ 1);
       else stage(cur ^ 1);
@@ -577,6 +607,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
     }
     vm_wait_all();
     __syncthreads();
+    if constexpr (DROPOUT) mw_cur = mw_nxt;
     if (++mt == n_mt) {
       mt = 0;
       ++g;
@@ -872,6 +903,20 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     inv_keep = 1.f / (1.f - p.dropout_p);
   }
 
+  // dropout keep words of this lane's row for the two 32-key halves of a tile (the forward's saved
+  // mask, tiled layout of fa2_amd.h), loaded one tile ahead: the loop's vm_wait_all retires them
+  uint32_t mwc[2] = {0u, 0u}, mwn[2] = {0u, 0u};
+  auto load_mw = [&](int n0, uint32_t* out) {
+    if constexpr (DROPOUT) {
+      if (p.dropout_mask) {
+        const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+        const int64_t rowbase = ((int64_t)(b * p.heads_q + hq) * nrb + (qi >> 5)) * ncw;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          out[t] = (qvalid && n0 + 32 * t < p.seqlen_k) ? p.dropout_mask[(rowbase + ((n0 >> 5) + t)) * 32 + (qi & 31)] : 0u;
+      }
+    }
+  };
   // one 64-key tile: S^T and dP^T for both 32-key halves first, then the softmax-gradient
   // VALU of each half beside the other half's MFMAs, then dQ^T += K^T dS^T.
   auto tile = [&](auto mask_c, const char* K, const char* V, int n0, bool later) {
@@ -923,8 +968,13 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
           if (DROPOUT) {  // dS = P (dP~ M / (1 - p) - delta), the forward's keep mask M
             // the forward's keep mask M (fully unrolled here: the rolled dropout_keep16 measured
             // 8 % slower in this kernel, which does not spill either way)
-            const uint64_t kjj = (uint64_t)(n0 + o + 4 * hh);
-            const bool keep = philox_uniform(p.dropout_seed, drop_row + kjj) > p.dropout_p;
+            bool keep;
+            if (p.dropout_mask) {  // the forward's saved bits (loaded a tile ahead)
+              keep = (mwc[t] >> ((i & 3) + 8 * (i >> 2) + 4 * hh)) & 1u;
+            } else {
+              const uint64_t kjj = (uint64_t)(n0 + o + 4 * hh);
+              keep = philox_uniform(p.dropout_seed, drop_row + kjj) > p.dropout_p;
+            }
             dsv[j] = pr * (dp[i] * (keep ? inv_keep : 0.f) - del_i);
           } else {
             dsv[j] = pr * (dp[i] - del_i);  // softmax_scale is applied to dQ once, at the end
@@ -1033,6 +1083,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     });
   };
 
+  load_mw(0, mwc);
   for (int it = 0; it < ntiles; ++it) {
     const int cur = it & 1;
     const int n0 = it * BN;
@@ -1040,6 +1091,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     // (the bias tile first: its counted wait leaves the next K/V tile in flight)
     if (!dead) bias_issue(n0);
     const bool later = it + 1 < ntiles;
+    if (DROPOUT && later) load_mw(n0 + BN, mwn);
     if (later) stage_kv(cur ^ 1, n0 + BN);
     const bool need_mask = (n0 + BN > Lk) || (mw0 + 31 >= Lq) || (CAUSAL && n0 + BN - 1 > mw0 + diag);
     if (!dead) {
@@ -1052,6 +1104,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
     }
     vm_wait_all();
     __syncthreads();
+    if constexpr (DROPOUT) {
+      mwc[0] = mwn[0];
+      mwc[1] = mwn[1];
+    }
   }
 
   if constexpr (ALIGNED && !DQF32) {
@@ -1233,6 +1289,11 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2
       const int rel = lim_lane - n0 - 4 * hh;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
+        uint32_t mwd = 0u;  // the forward's saved keep word of this row and key half
+        if (DROPOUT && p.dropout_mask && qvalid && n0 + 32 * t < p.seqlen_k) {
+          const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+          mwd = p.dropout_mask[((((int64_t)(b * p.heads_q + hq) * nrb + (qi >> 5)) * ncw + ((n0 >> 5) + t)) * 32) + (qi & 31)];
+        }
         f32x16 s = zero16(), dp = zero16();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -1250,7 +1311,8 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2
           pr = o < rel ? pr : 0.f;
           float dpv = dp[i];
           if (DROPOUT) {
-            const bool keep = philox_uniform(p.dropout_seed, drop_row + (uint64_t)kj) > p.dropout_p;
+            const bool keep = p.dropout_mask ? ((mwd >> ((i & 3) + 8 * (i >> 2) + 4 * hh)) & 1u) != 0
+                                             : philox_uniform(p.dropout_seed, drop_row + (uint64_t)kj) > p.dropout_p;
             dpv *= keep ? inv_keep : 0.f;
           }
           ds[i] = pr * (dpv + ndel);

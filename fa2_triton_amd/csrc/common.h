@@ -510,6 +510,24 @@ FA2_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// 32 x 32 bit-matrix transpose across each 32-lane half: lane r holds row r (bit k = element
+// (r, k)); afterwards lane k holds column k (bit r = element (r, k)).  Five xor stages of
+// ds_swizzle (bitmask mode, no LDS access); every lane of the wave must be active.
+template <int J>
+FA2_DEV uint32_t transpose32_stage(uint32_t x, int r32) {
+  constexpr uint32_t m = J == 16 ? 0x0000FFFFu : J == 8 ? 0x00FF00FFu : J == 4 ? 0x0F0F0F0Fu : J == 2 ? 0x33333333u : 0x55555555u;
+  const uint32_t y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
+  return (r32 & J) ? (((y >> J) & m) | (x & ~m)) : ((x & m) | ((y & m) << J));
+}
+FA2_DEV uint32_t transpose32_lanes(uint32_t x, int r32) {
+  x = transpose32_stage<16>(x, r32);
+  x = transpose32_stage<8>(x, r32);
+  x = transpose32_stage<4>(x, r32);
+  x = transpose32_stage<2>(x, r32);
+  return transpose32_stage<1>(x, r32);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Philox4x32-10, first output word, counter (lo, hi, 0, 0), key (seed_lo, seed_hi), converted
 // to [0,1) exactly like Triton's tl.rand (triton/language/random.py:13-156; see
 // oracle/philox.py).  Used for the forward dropout mask keep = rand > p

@@ -24,8 +24,6 @@
 #include "common.h"
 #include "fa2_internal.h"
 #include "fwd_pipe_kernel.h"
-#include "fwd_w64_kernel.h"
-#include <stdlib.h>
 
 namespace fa2 {
 
@@ -207,11 +205,23 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
       }
       if (DROPOUT) {
         const uint64_t rowoff = drop_base + (uint64_t)qi * Lk;
+        uint32_t kb = 0;  // keep bits of this lane's 16 keys at their positions in the 32-key word
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int kj = n0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const float u = philox_uniform(p.dropout_seed, rowoff + kj);
-          pv[i] = u > p.dropout_p ? pv[i] : 0.f;
+          const bool keep = philox_uniform(p.dropout_seed, rowoff + kj) > p.dropout_p;
+          pv[i] = keep ? pv[i] : 0.f;
+          kb |= (uint32_t)keep << ((i & 3) + 8 * (i >> 2) + 4 * hh);
+        }
+        if (p.dropout_mask) {
+          // the row's 32-key word = this lane's bits | the partner lane's (l ^ 32, same row);
+          // lanes of half t store it: word (qi, key word (n0 + 32 t) / 32) of the tiled layout
+          const auto r = __builtin_amdgcn_permlane32_swap(kb, kb, false, false);
+          if (hh == t && qi < p.seqlen_q && n0 + 32 * t < p.seqlen_k) {
+            const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+            const int64_t wi = (((int64_t)bh * nrb + (qi >> 5)) * ncw + ((n0 + 32 * t) >> 5)) * 32 + (qi & 31);
+            p.dropout_mask[wi] = r[0] | r[1];
+          }
         }
       }
 #pragma unroll
@@ -390,10 +400,6 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   if constexpr (DT == 64 || DT == 128) {
     const bool bias16 = bias16_rows(a.bias, a.bias_dtype, a.bias_stride);
     if (aligned && !dr && a.k_stride[1] == a.v_stride[1] && (!bi || bias16)) {
-      if constexpr (DT == 128) {
-        static const bool w64 = getenv("FA2_FWD_W64") && atoi(getenv("FA2_FWD_W64")) != 0;
-        if (!bi && w64) return c ? launch_fwd_w64<BF16, DT, true>(a, st) : launch_fwd_w64<BF16, DT, false>(a, st);
-      }
       if (!bi) return c ? launch_fwd_pipe<BF16, DT, true, 0>(a, st) : launch_fwd_pipe<BF16, DT, false, 0>(a, st);
       if (a.bias_dtype == FA2_BF16)
         return c ? launch_fwd_pipe<BF16, DT, true, 17>(a, st) : launch_fwd_pipe<BF16, DT, false, 17>(a, st);

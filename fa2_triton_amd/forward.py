@@ -4,7 +4,9 @@
 dropout_seed) -> (o, lse, softmax_scale, dropout_seed)`; q [B, Sq, Hq, D], k/v [B, Sk, Hkv, D],
 lse [B, Hq, ceil(Sq/128)*128] fp32 in base-2 units.  The Triton launch (:83-116) becomes one
 call of the C ABI `fa2_fwd`; the varlen pack/unpack (:44-63, :118-120) disappears because the
-HIP kernel reads the padded tensors in place using device-side cu_seqlens.
+HIP kernel reads the padded tensors in place using device-side cu_seqlens.  Keyword-only
+`dropout_mask` (beyond the reference): an int32 buffer of dropout_mask_words(...) words that the
+forward fills with the keep bits it drew, for the backward to read instead of regenerating them.
 """
 import ctypes
 import math
@@ -14,7 +16,8 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .utils import bshd_strides, cu_seqlens_from_mask, encode_dtype, handle_dropout, infer_bias_strides, launch_on
+from .utils import (bshd_strides, check_dropout_mask, cu_seqlens_from_mask, encode_dtype, handle_dropout,
+                    infer_bias_strides, launch_on)
 
 
 def _flash_attn_forward(
@@ -27,6 +30,8 @@ def _flash_attn_forward(
     causal: bool = False,
     softmax_scale: Optional[float] = None,
     dropout_seed: Optional[int] = None,
+    *,
+    dropout_mask: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor, float, int]:
     if attention_mask is not None:
         assert bias is None, "Attention mask is not supported along with attention bias. Just use bias instead."
@@ -71,6 +76,9 @@ def _flash_attn_forward(
     args.softmax_scale = float(softmax_scale)
     args.dropout_p = float(dropout_p)
     args.dropout_seed = int(dropout_seed) & 0xFFFFFFFFFFFFFFFF
+    if dropout_mask is not None and dropout_p > 0.0:
+        check_dropout_mask(dropout_mask, batch, nheads_q, seqlen_q, seqlen_k, q.device)
+        args.dropout_mask = dropout_mask.data_ptr()
     lib = _lib.load()
     _lib.check(launch_on(q, lambda st: lib.fa2_fwd(ctypes.byref(args), st)))
     return o, lse, softmax_scale, dropout_seed

@@ -43,6 +43,19 @@ def infer_bias_strides(
     return stride_bb, stride_bh, bias.stride(2)
 
 
+def dropout_mask_words(batch: int, heads_q: int, seqlen_q: int, seqlen_k: int) -> int:
+    """int32 words of a dropout keep mask (fa2_dropout_mask_bytes / 4 in include/fa2_amd.h):
+    32 x 32 bit tiles, batch * heads_q * ceil(Sq / 32) * ceil(Sk / 32) * 32 words."""
+    return batch * heads_q * ((seqlen_q + 31) // 32) * ((seqlen_k + 31) // 32) * 32
+
+
+def check_dropout_mask(mask: torch.Tensor, batch: int, heads_q: int, seqlen_q: int, seqlen_k: int, device) -> None:
+    need = dropout_mask_words(batch, heads_q, seqlen_q, seqlen_k)
+    assert mask.dtype == torch.int32 and mask.is_contiguous() and mask.device == device, \
+        "dropout_mask must be a contiguous int32 tensor on the inputs' device"
+    assert mask.numel() >= need, f"dropout_mask has {mask.numel()} words, {need} needed"
+
+
 def handle_dropout(dropout_p: float, dropout_seed: Optional[int], is_forward: bool) -> int:
     """Seed handling of /root/reference/src/utils.py:80-88.
 

@@ -5,8 +5,10 @@ causal=False, softmax_scale=None, dropout_seed=None)` with q [B, Sq, Hq, D], k/v
 [B, Sk, Hkv, D] (fp16 / bf16), returns O [B, Sq, Hq, D].  Backward returns (dq, dk, dv) and
 no gradient for the mask and scalars, exactly as the reference (:62-86).  Beyond the
 reference (which returns None for the bias, :86): when `attention_bias` requires grad, its
-gradient dL/d(bias) is returned too.
+gradient dL/d(bias) is returned too.  With dropout the keep
+bits drawn by the forward are kept for the backward (see _keep_mask_buffer).
 """
+import os
 from typing import Optional
 
 import torch
@@ -14,6 +16,19 @@ from torch import Tensor
 
 from .backward import _flash_attn_backward
 from .forward import _flash_attn_forward
+from .utils import dropout_mask_words
+
+
+def _keep_mask_buffer(q: Tensor, k: Tensor, v: Tensor, dropout_p: float) -> Optional[Tensor]:
+    """With dropout, the forward saves its keep bits (1 bit per score, include/fa2_amd.h) so
+    that the backward reads them instead of drawing Philox twice more (dQ and dK/dV).  Above
+    FA2_DROPOUT_MASK_MAX_GB (default 4) the backward regenerates them instead."""
+    if not dropout_p > 0.0 or not (q.requires_grad or k.requires_grad or v.requires_grad):  # (inputs of Function.forward)
+        return None
+    words = dropout_mask_words(q.size(0), q.size(2), q.size(1), k.size(1))
+    if words * 4 > float(os.environ.get("FA2_DROPOUT_MASK_MAX_GB", "4")) * 2**30:
+        return None
+    return torch.empty(words, dtype=torch.int32, device=q.device)
 
 
 class FlashAttnFunc(torch.autograd.Function):
@@ -35,6 +50,7 @@ class FlashAttnFunc(torch.autograd.Function):
         k = k if k.stride(-1) == 1 else k.contiguous()
         v = v if v.stride(-1) == 1 else v.contiguous()
         attention_bias = None if attention_bias is None else attention_bias.contiguous()
+        ctx.dropout_mask = _keep_mask_buffer(q, k, v, dropout_p)
         o, lse, ctx.softmax_scale, ctx.dropout_seed = _flash_attn_forward(
             q=q,
             k=k,
@@ -45,6 +61,7 @@ class FlashAttnFunc(torch.autograd.Function):
             causal=causal,
             softmax_scale=softmax_scale,
             dropout_seed=dropout_seed,
+            dropout_mask=ctx.dropout_mask,
         )
         ctx.save_for_backward(q, k, v, attention_bias, attention_mask, o, lse)
         ctx.causal = causal
@@ -69,6 +86,7 @@ class FlashAttnFunc(torch.autograd.Function):
             softmax_scale=ctx.softmax_scale,
             dropout_seed=ctx.dropout_seed,
             bias_grad=bias_grad,
+            dropout_mask=ctx.dropout_mask,
         )
         dbias = grads[3] if bias_grad else None
         return grads[0], grads[1], grads[2], None, dbias, None, None, None, None

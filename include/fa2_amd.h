@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 5
+#define FA2_ABI_VERSION 6
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -68,12 +68,20 @@ typedef struct fa2_fwd_args {
   float softmax_scale;
   float dropout_p;        /* 0 <= p < 1 */
   uint64_t dropout_seed;  /* Philox4x32-10 key, identical to Triton's tl.rand */
+  /* optional dropout keep mask out (ABI 6): when non-NULL and dropout_p > 0, the forward also
+   * writes the keep bits it drew (keep = tl.rand > p) into this buffer of
+   * fa2_dropout_mask_bytes(batch, heads_q, seqlen_q, seqlen_k) bytes, so that the backward reads
+   * them instead of regenerating Philox (fa2_bwd_args.dropout_mask).  Layout: 32 x 32 bit tiles,
+   * word[((b * Hq + h) * ceil(Sq / 32) + i / 32) * ceil(Sk / 32) + j / 32][i % 32], bit j % 32 =
+   * keep(b, h, i, j).  Only the tiles the (causal) mask leaves visible are written. */
+  uint32_t* dropout_mask;
 } fa2_fwd_args;
 
 /* Backward: dQ, dK, dV of the forward above.  dK/dV are written with heads_kv heads: the GQA
  * group sum is done in fp32 inside the kernel.  dropout_p > 0 is supported (the reference
- * raises NotImplementedError, /root/reference/src/utils.py:80-88): the kernels regenerate the
- * forward's Philox keep mask, so dropout_p and dropout_seed must equal the forward's. */
+ * raises NotImplementedError, /root/reference/src/utils.py:80-88): the kernels read the keep
+ * mask the forward saved (dropout_mask) or regenerate it with Philox, so dropout_p and
+ * dropout_seed must equal the forward's. */
 typedef struct fa2_bwd_args {
   const void* q;
   const void* k;
@@ -124,6 +132,10 @@ typedef struct fa2_bwd_args {
    * host, /root/reference/src/backward/caller.py:118-121,162-165).  Contents are scratch. */
   float* dkv_workspace;
   int64_t dkv_workspace_bytes;
+  /* optional (ABI 6): the keep mask a forward with the same dropout_p / dropout_seed wrote
+   * (fa2_fwd_args.dropout_mask); NULL = regenerate it with Philox (dQ, dK/dV and the bias
+   * gradient each draw it again). */
+  const uint32_t* dropout_mask;
 } fa2_bwd_args;
 
 int fa2_fwd(const fa2_fwd_args* args, void* stream);
@@ -141,6 +153,8 @@ int fa2_bwd_stages(const fa2_bwd_args* args, int stages, void* stream);
  * that gives at least 512 dK/dV workgroups (two per CU), or 0 when no split applies (Hq == Hkv,
  * or the grid is already that large). */
 int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* args);
+/* Bytes of a dropout keep mask (ABI 6): batch * heads_q * ceil(seqlen_q / 32) * ceil(seqlen_k / 32) * 128. */
+int64_t fa2_dropout_mask_bytes(int32_t batch, int32_t heads_q, int32_t seqlen_q, int32_t seqlen_k);
 
 /* cu_seqlens[0] = 0, cu_seqlens[b+1] = cu_seqlens[b] + sum_s mask[b, s]  (mask: uint8/bool,
  * row stride mask_row_stride bytes).  Replaces attention_mask.sum(1).cumsum(0) and the

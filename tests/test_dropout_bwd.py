@@ -1,8 +1,9 @@
 """Backward with dropout -- SURVEY.md section 8(f) rank 2 (the reference raises, src/utils.py:88).
 
-The forward draws its keep mask with Philox (tl.rand semantics, oracle/philox.py); the backward
-kernels regenerate the same bits from the seed the forward returned and differentiate
-O = (P * M / (1 - p)) V exactly.  The oracle applies the identical mask (dropout_keep_mask_torch),
+The forward draws its keep mask with Philox (tl.rand semantics, oracle/philox.py) and, through the
+autograd op, saves the bits (ABI 6 keep mask); the backward kernels read them -- or, without a
+saved mask, regenerate the same bits from the seed -- and differentiate O = (P * M / (1 - p)) V
+exactly.  The oracle applies the identical mask (dropout_keep_mask_torch),
 so the acceptance rule is the reference tests' compare_results_fa on O, dQ, dK, dV, as for the
 no-dropout grid.  Also checked: two backward passes from the same forward are bitwise equal.
 """
@@ -39,3 +40,68 @@ def test_dropout_backward_is_deterministic():
     g2 = torch.autograd.grad(out, (q, k, v), do)
     for a, b_ in zip(g1, g2):
         assert torch.equal(a, b_)
+
+
+def _unpack_keep_mask(words, b, h, sq, sk):
+    """Dense [B, Hq, Sq, Sk] bool view of the tiled keep mask of include/fa2_amd.h (ABI 6)."""
+    nrb, ncw = (sq + 31) // 32, (sk + 31) // 32
+    t = words.view(b, h, nrb, ncw, 32)  # [.., row tile, key word, row in tile]
+    bits = (t.unsqueeze(-1) >> torch.arange(32, device=words.device, dtype=torch.int32)) & 1
+    dense = bits.permute(0, 1, 2, 4, 3, 5).reshape(b, h, nrb * 32, ncw * 32)
+    return dense[:, :, :sq, :sk].bool()
+
+
+MASK_CASES = [
+    # b, hq, hkv, sq, sk, d, causal, p, dtype
+    (2, 4, 2, 239, 301, 128, True, 0.17, torch.bfloat16),
+    (3, 2, 2, 127, 513, 64, False, 0.1, torch.float16),
+    (2, 8, 2, 1024, 1024, 128, True, 0.1, torch.bfloat16),
+    (1, 2, 2, 333, 200, 96, True, 0.25, torch.bfloat16),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,d,causal,p,dtype", MASK_CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_saved_keep_mask_matches_philox_and_regeneration(b, hq, hkv, sq, sk, d, causal, p, dtype):
+    """The forward's saved keep bits equal the oracle's Philox mask on every visible element, and a
+    backward that reads them is bitwise equal to one that regenerates them (dQ, dK, dV, dBias)."""
+    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from fa2_triton_amd.utils import dropout_mask_words
+    from oracle.philox import dropout_keep_mask_torch
+
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, d, dtype)
+    seed = 1234
+    words = torch.full((dropout_mask_words(b, hq, sq, sk),), -1, dtype=torch.int32, device=q.device)
+    o, lse, scale, seed = _flash_attn_forward(q, k, v, None, None, p, causal, None, seed, dropout_mask=words)
+    o_ref, _, _, _ = _flash_attn_forward(q, k, v, None, None, p, causal, None, seed)
+    assert torch.equal(o, o_ref)  # writing the mask does not change the forward
+    keep = _unpack_keep_mask(words, b, hq, sq, sk)
+    want = dropout_keep_mask_torch(seed, p, b, hq, sq, sk, device=q.device)
+    vis = torch.ones(sq, sk, dtype=torch.bool, device=q.device)
+    if causal:  # bottom-right aligned: key j visible to row i iff j <= i + sk - sq
+        vis = torch.arange(sk, device=q.device)[None, :] <= torch.arange(sq, device=q.device)[:, None] + (sk - sq)
+    assert torch.equal(keep[:, :, vis], want[:, :, vis])
+    bias = (torch.randn(1, hq, sq, sk, device=q.device) * 0.5).to(dtype)
+    for bb in (None, bias):
+        o2, lse2, _, _ = _flash_attn_forward(q, k, v, None, bb, p, causal, None, seed, dropout_mask=words)
+        g_mask = _flash_attn_backward(do, q, k, v, bb, None, o2, lse2, p, causal, scale, seed,
+                                      bias_grad=bb is not None, dropout_mask=words)
+        g_regen = _flash_attn_backward(do, q, k, v, bb, None, o2, lse2, p, causal, scale, seed,
+                                       bias_grad=bb is not None)
+        for x, y in zip(g_mask, g_regen):
+            if x is not None:
+                assert torch.equal(x, y)
+
+
+def test_keep_mask_layout_unpacks_a_known_pattern():
+    """CPU check of the tiled layout helper: bit j % 32 of word [bh][i/32][j/32][i % 32]."""
+    b, h, sq, sk = 1, 2, 40, 70
+    nrb, ncw = 2, 3
+    words = torch.zeros(b * h * nrb * ncw * 32, dtype=torch.int32)
+    dense = torch.zeros(b, h, sq, sk, dtype=torch.bool)
+    for (hh, i, j) in [(0, 0, 0), (1, 39, 69), (0, 33, 31), (1, 5, 64)]:
+        dense[0, hh, i, j] = True
+        wi = ((hh * nrb + i // 32) * ncw + j // 32) * 32 + i % 32
+        words[wi] |= torch.tensor(1 << (j % 32), dtype=torch.int64).to(torch.int32)
+    assert torch.equal(_unpack_keep_mask(words, b, h, sq, sk), dense)
