@@ -517,7 +517,9 @@ template <int J>
 FA2_DEV uint32_t transpose32_stage(uint32_t x, int r32) {
   constexpr uint32_t m = J == 16 ? 0x0000FFFFu : J == 8 ? 0x00FF00FFu : J == 4 ? 0x0F0F0F0Fu : J == 2 ? 0x33333333u : 0x55555555u;
   const uint32_t y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
-  return (r32 & J) ? (((y >> J) & m) | (x & ~m)) : ((x & m) | ((y & m) << J));
+  // branch-free select on the lane bit (a ternary here compiles to five divergent branches)
+  const uint32_t hi = 0u - (uint32_t)((r32 >> __builtin_ctz(J)) & 1);
+  return ((((y >> J) & m) | (x & ~m)) & hi) | (((x & m) | ((y & m) << J)) & ~hi);
 }
 FA2_DEV uint32_t transpose32_lanes(uint32_t x, int r32) {
   x = transpose32_stage<16>(x, r32);
