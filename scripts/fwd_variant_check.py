@@ -30,6 +30,7 @@ shapes = [  # B, Hq, Hkv, Sq, Sk, D, causal
     (2, 3, 3, 300, 777, 128, True), (2, 3, 3, 777, 300, 128, True), (2, 3, 3, 777, 300, 128, False),
     (1, 2, 1, 1, 513, 128, True), (1, 2, 2, 257, 257, 128, True), (3, 2, 2, 64, 64, 128, False),
     (1, 2, 2, 8192, 8192, 128, True),
+    (2, 4, 4, 1024, 1024, 64, False), (1, 4, 2, 777, 513, 64, False), (2, 2, 2, 100, 1000, 64, True),
 ]
 worst = 0.0
 for dt in (torch.bfloat16, torch.float16):
