@@ -327,8 +327,8 @@ __global__ void __launch_bounds__(NW * 64, DT <= 64 && !CAUSAL && NW == 4 && BIA
       }
 #pragma unroll
       for (int e = 0; e < EPS; e += 2) exp_pair(cur, m * EPS + e, rs0, rs1);
-      // the row-sum adds stay in this step: left alone, IR sinking moves all 32 to the end of the
-      // phase as two serial chains beside the last MFMA (sched_barrier does not bind IR passes)
+      // the row-sum adds stay in this step: left alone, the compiler moves all 32 to the end of the
+      // phase as two serial chains beside the last MFMA (sched_barrier does not bind that motion)
       asm volatile("" : "+v"(rs0), "+v"(rs1));
       if (m % kEveryX == 0 && m / kEveryX < kPerX) dma(i, m / kEveryX);
       __builtin_amdgcn_sched_barrier(0);
