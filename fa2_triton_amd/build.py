@@ -53,8 +53,20 @@ def generated_sources():
     return srcs
 
 
+def generated_headers():
+    """The hand-placed instruction streams (hp_gen.py -> csrc/gen/*.h), rewritten only on change."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    try:
+        from fa2_triton_amd import hp_gen
+    finally:
+        sys.path.pop(0)
+    return [hp_gen.write_headers()]
+
+
 def deps_mtime() -> float:
     files = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))]
+    files += [os.path.join(GEN, f) for f in os.listdir(GEN) if f.endswith(".h")]
+    files.append(os.path.join(HERE, "hp_gen.py"))
     files.append(os.path.join(INCLUDE, "fa2_amd.h"))
     files.append(os.path.abspath(__file__))
     return max(os.path.getmtime(f) for f in files)
@@ -87,6 +99,7 @@ def compile_one(src: str, force: bool, dep_t: float) -> str:
 
 def build(force: bool = False, jobs: int = 0) -> str:
     os.makedirs(OBJ, exist_ok=True)
+    generated_headers()
     srcs = [os.path.join(CSRC, "api.hip"), os.path.join(CSRC, "misc.hip")] + generated_sources()
     dep_t = deps_mtime()
     jobs = jobs or min(16, os.cpu_count() or 4)

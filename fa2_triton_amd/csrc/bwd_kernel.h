@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dkdv_kernel(const fa2_
   auto bias_issue = [&](int hq_, int m_) {
     if constexpr (BIASL) {
       const uint16_t* bg = (const uint16_t*)p.bias + b * p.bias_stride[0] + hq_ * p.bias_stride[1] + kw0;
-      const i32x4 r = BiasStager::tile_rsrc(bg, p.bias_stride[2], m_, p.seqlen_q, brows);
+      const i32x4 r = bias_tile_rsrc(bg, p.bias_stride[2], m_, p.seqlen_q, brows, p.seqlen_k - kw0, 32);
 #pragma unroll
       for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bwk, r, it);
     }
@@ -825,7 +825,7 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
   }
   auto bias_issue = [&](int n) {
     if constexpr (BIASL) {
-      const i32x4 r = BiasStager::tile_rsrc(bg + n, p.bias_stride[2], mw0, p.seqlen_q, brows);
+      const i32x4 r = bias_tile_rsrc(bg + n, p.bias_stride[2], mw0, p.seqlen_q, brows, p.seqlen_k - n, 64);
 #pragma unroll
       for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bw, r, it);
     }

@@ -358,6 +358,20 @@ FA2_DEV i32x4 make_rsrc(const void* base, uint32_t n) {
   return r;
 }
 
+// Descriptor of a 16-bit bias tile [rows from row0][tile_keys keys] whose key 0 is element g of
+// row 0 (row stride `stride` elements, a multiple of 8 -- bias16_rows).  The range ends at the
+// last valid key of the last valid row, rounded up to a whole 16-byte chunk (which a 16-byte
+// aligned row always holds): pieces for keys past seqlen_k of the final row read as zeros
+// instead of past the end of the tensor.  keys_left = seqlen_k - (first key of the tile).
+// Rows past row_end read as zeros as in BufStager::tile_rsrc.
+FA2_DEV i32x4 bias_tile_rsrc(const uint16_t* g, int64_t stride, int row0, int row_end, int max_rows, int keys_left,
+                             int tile_keys) {
+  const int rows = min(max(row_end - row0, 0), max_rows);
+  const int kv = min(max((keys_left + 7) & ~7, 0), tile_keys);
+  const uint32_t n = (rows > 0 && kv > 0) ? (uint32_t)(rows - 1) * (uint32_t)(stride * 2) + (uint32_t)kv * 2u : 0u;
+  return make_rsrc(g + (int64_t)row0 * stride, n);
+}
+
 // One dword per lane by buffer LDS-DMA (buffer_load_dword ... lds): LDS destination =
 // lds_base_uniform + 4 * lane (active lanes), source = descriptor base + voff bytes.
 FA2_DEV void blds4(uint32_t voff, i32x4 rsrc, uint32_t lds_base_uniform) {

@@ -19,10 +19,13 @@
 // fragment reads overlap its partner's MFMAs, instead of both waves hitting LDS, MFMA and VALU
 // in lockstep.  K_{i+1} is issued at the start of A_i and V_{i+1} at the start of B_i (each
 // two phases ahead of its first reader), retired by counted vmcnt waits before the barriers.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
 #include "fa2_internal.h"
+#include "fwd_hp_kernel.h"
 #include "fwd_pipe_kernel.h"
 
 namespace fa2 {
@@ -397,6 +400,10 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   const bool c = a.causal != 0, bi = a.bias != nullptr, dr = a.dropout_p > 0.f;
   // hot path: software-pipelined kernel (fwd_pipe_kernel.h), also with a 16-bit bias whose rows
   // are 16-byte aligned (its tiles are staged by LDS-DMA)
+  if constexpr (DT == 128) {
+    // hand-placed one-wave-per-SIMD kernel (fwd_hp_kernel.h) for D = 128 exactly
+    if (fwd_hp_ok(a, aligned)) return c ? launch_fwd_hp<BF16, true>(a, st) : launch_fwd_hp<BF16, false>(a, st);
+  }
   if constexpr (DT == 64 || DT == 128) {
     const bool bias16 = bias16_rows(a.bias, a.bias_dtype, a.bias_stride);
     if (aligned && !dr && a.k_stride[1] == a.v_stride[1] && (!bi || bias16)) {

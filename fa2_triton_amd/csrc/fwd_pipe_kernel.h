@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(NW * 64, DT <= 64 && !CAUSAL && NW == 4 && BIA
   }
   auto bias_issue = [&](int t) {
     if constexpr (BIAS) {
-      const i32x4 r = BiasStager::tile_rsrc(bg + t * BN, p.bias_stride[2], qw0, p.seqlen_q, brows);
+      const i32x4 r = bias_tile_rsrc(bg + t * BN, p.bias_stride[2], qw0, p.seqlen_q, brows, p.seqlen_k - t * BN, BN);
 #pragma unroll
       for (int it = 0; it < BiasStager::kIters; ++it) bst.piece(bw, r, it);
     }

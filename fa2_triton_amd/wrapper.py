@@ -8,6 +8,7 @@ reference (which returns None for the bias, :86): when `attention_bias` requires
 gradient dL/d(bias) is returned too.  With dropout the keep
 bits drawn by the forward are kept for the backward (see _keep_mask_buffer).
 """
+import logging
 import os
 from typing import Optional
 
@@ -22,13 +23,20 @@ from .utils import dropout_mask_words
 def _keep_mask_buffer(q: Tensor, k: Tensor, v: Tensor, dropout_p: float) -> Optional[Tensor]:
     """With dropout, the forward saves its keep bits (1 bit per score, include/fa2_amd.h) so
     that the backward reads them instead of drawing Philox twice more (dQ and dK/dV).  Above
-    FA2_DROPOUT_MASK_MAX_GB (default 4) the backward regenerates them instead."""
+    FA2_DROPOUT_MASK_MAX_GB (default 4, per call), or when the allocation itself fails, the
+    backward regenerates them instead (bitwise the same gradients, tests/test_dropout_bwd.py):
+    the mask is an O(S^2) cache, never a reason for a forward that fits in O(S) memory to fail."""
     if not dropout_p > 0.0 or not (q.requires_grad or k.requires_grad or v.requires_grad):  # (inputs of Function.forward)
         return None
     words = dropout_mask_words(q.size(0), q.size(2), q.size(1), k.size(1))
     if words * 4 > float(os.environ.get("FA2_DROPOUT_MASK_MAX_GB", "4")) * 2**30:
         return None
-    return torch.empty(words, dtype=torch.int32, device=q.device)
+    try:
+        return torch.empty(words, dtype=torch.int32, device=q.device)
+    except torch.OutOfMemoryError:
+        logging.getLogger(__name__).info("dropout keep mask (%d bytes) not allocated: the backward regenerates it",
+                                         words * 4)
+        return None
 
 
 class FlashAttnFunc(torch.autograd.Function):

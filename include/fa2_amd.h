@@ -134,7 +134,10 @@ typedef struct fa2_bwd_args {
   int64_t dkv_workspace_bytes;
   /* optional (ABI 6): the keep mask a forward with the same dropout_p / dropout_seed wrote
    * (fa2_fwd_args.dropout_mask); NULL = regenerate it with Philox (dQ, dK/dV and the bias
-   * gradient each draw it again). */
+   * gradient each draw it again).  The backward kernels may READ words the forward never wrote
+   * (tiles the causal mask hides, prefetches one tile past the last live one): such a word only
+   * ever gates a (row, key) pair whose probability is 0, so its contents never reach a result and
+   * the buffer needs no initialisation. */
   const uint32_t* dropout_mask;
 } fa2_bwd_args;
 

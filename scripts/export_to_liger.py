@@ -31,29 +31,35 @@ def export(liger_root: str, with_lib: bool = True, force: bool = False) -> list:
     unless `force`, and even then only overwritten file by file, never deleted."""
     dst = os.path.join(liger_root, FA_DIR_IN_LIGER)
     manifest = os.path.join(dst, MANIFEST)
+    root = os.path.realpath(dst)
     if os.path.exists(manifest):
         for rel in open(manifest).read().split():
-            path = os.path.join(dst, rel)
-            if os.path.isfile(path):
+            path = os.path.realpath(os.path.join(dst, rel))
+            # only files inside the export directory: an absolute or '..' entry is ignored
+            if os.path.commonpath([root, path]) == root and path != root and os.path.isfile(path):
                 os.remove(path)
     elif os.path.exists(dst) and os.listdir(dst) and not force:
         raise SystemExit(f"{dst} exists and was not written by this script; pass --force to overwrite files in it")
     os.makedirs(os.path.join(dst, "csrc"), exist_ok=True)
     os.makedirs(os.path.join(dst, "include"), exist_ok=True)
-    written = []
+    written, adopted = [], []
+
+    def put(src, path):
+        # a file that was there before this export (someone else's, reachable only with --force) is
+        # overwritten but not adopted into the manifest, so a later refresh never deletes it
+        (adopted if os.path.exists(path) else written).append(path)
+        shutil.copy2(src, path)
+
     for name in sorted(os.listdir(PKG)):
         if name.endswith(".py") or (with_lib and name == "libfa2_amd.so"):
-            shutil.copy2(os.path.join(PKG, name), os.path.join(dst, name))
-            written.append(os.path.join(dst, name))
+            put(os.path.join(PKG, name), os.path.join(dst, name))
     for name in sorted(os.listdir(os.path.join(PKG, "csrc"))):
         if name.endswith((".h", ".hip")):  # generated per-instantiation units are rebuilt by build.py
-            shutil.copy2(os.path.join(PKG, "csrc", name), os.path.join(dst, "csrc", name))
-            written.append(os.path.join(dst, "csrc", name))
-    shutil.copy2(os.path.join(ROOT, "include", "fa2_amd.h"), os.path.join(dst, "include", "fa2_amd.h"))
-    written.append(os.path.join(dst, "include", "fa2_amd.h"))
+            put(os.path.join(PKG, "csrc", name), os.path.join(dst, "csrc", name))
+    put(os.path.join(ROOT, "include", "fa2_amd.h"), os.path.join(dst, "include", "fa2_amd.h"))
     with open(manifest, "w") as f:
         f.write("\n".join(os.path.relpath(p, dst) for p in written) + "\n")
-    return written
+    return written + adopted
 
 
 def main(argv=None):

@@ -1,0 +1,57 @@
+"""GPU dev check of the hand-placed forward (fwd_hp_kernel) against fwd_pipe_kernel and the oracle.
+
+For each shape: O and LSE2 from FA2_FWD_HP=1 and =0 in one process, max |diff| between them, and
+each one's max |O - O_fp32 oracle|.  usage: python tests/hp_check.py
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
+from oracle.reference import attention_reference  # noqa: E402
+
+CASES = [
+    # b, hq, hkv, sq, sk, causal, dtype
+    (1, 1, 1, 256, 256, False, torch.bfloat16),
+    (1, 1, 1, 256, 256, True, torch.bfloat16),
+    (2, 4, 2, 512, 512, True, torch.bfloat16),
+    (2, 4, 4, 1024, 1024, False, torch.float16),
+    (1, 2, 1, 300, 700, True, torch.bfloat16),
+    (1, 2, 2, 777, 333, True, torch.float16),
+    (1, 2, 2, 1, 129, False, torch.bfloat16),
+    (2, 8, 8, 2048, 2048, True, torch.bfloat16),
+]
+
+
+def run(case):
+    b, hq, hkv, sq, sk, causal, dt = case
+    torch.manual_seed(0)
+    q = torch.randn(b, sq, hq, 128, device="cuda", dtype=dt) * 0.5
+    k = torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5
+    v = torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5
+    res = {}
+    for hp in ("1", "0"):
+        os.environ["FA2_FWD_HP"] = hp
+        o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        torch.cuda.synchronize()
+        res[hp] = (o.float(), lse[:, :, :sq].float())
+    ref = attention_reference(q, k, v, causal=causal).float()
+    pt = attention_reference(q, k, v, causal=causal, upcast=False, reorder_ops=True).float()
+    d_o = (res["1"][0] - res["0"][0]).abs().max().item()
+    fin = torch.isfinite(res["0"][1])
+    d_l = (res["1"][1][fin] - res["0"][1][fin]).abs().max().item() if fin.any() else 0.0
+    same_inf = torch.equal(torch.isfinite(res["1"][1]), fin)
+    e1 = (res["1"][0] - ref).abs().max().item()
+    e0 = (res["0"][0] - ref).abs().max().item()
+    ept = (pt - ref).abs().max().item()
+    ok = e1 <= 2 * ept + 5e-5 and same_inf
+    print(f"{case}: hp-pipe |dO| {d_o:.3e} |dLSE2| {d_l:.3e} inf-pattern {same_inf} | err hp {e1:.3e} pipe {e0:.3e} "
+          f"pt {ept:.3e} {'OK' if ok else 'FAIL'}", flush=True)
+    return ok
+
+
+if __name__ == "__main__":
+    bad = [c for c in CASES if not run(c)]
+    sys.exit(1 if bad else 0)

@@ -105,3 +105,88 @@ def test_keep_mask_layout_unpacks_a_known_pattern():
         wi = ((hh * nrb + i // 32) * ncw + j // 32) * 32 + i % 32
         words[wi] |= torch.tensor(1 << (j % 32), dtype=torch.int64).to(torch.int32)
     assert torch.equal(_unpack_keep_mask(words, b, h, sq, sk), dense)
+
+
+def test_keep_mask_allocation_falls_back_on_oom(monkeypatch):
+    """CPU: an OutOfMemoryError while allocating the keep mask means 'no saved mask' (the backward
+    regenerates the bits), never a failed forward (the mask is O(S^2) per call)."""
+    from fa2_triton_amd import wrapper
+
+    q = torch.zeros(1, 64, 2, 16, requires_grad=True)
+    k = torch.zeros(1, 64, 2, 16, requires_grad=True)
+    assert wrapper._keep_mask_buffer(q, k, k, 0.1) is not None
+
+    def oom(*a, **kw):
+        raise torch.OutOfMemoryError("forced")
+
+    monkeypatch.setattr(wrapper.torch, "empty", oom)
+    assert wrapper._keep_mask_buffer(q, k, k, 0.1) is None
+    monkeypatch.undo()
+    monkeypatch.setenv("FA2_DROPOUT_MASK_MAX_GB", "0")
+    assert wrapper._keep_mask_buffer(q, k, k, 0.1) is None
+
+
+@pytest.mark.gpu
+def test_forced_mask_fallback_gives_bitwise_equal_gradients(monkeypatch):
+    """The autograd op with its keep-mask allocation failing (forced OOM) returns the same O and
+    bitwise the same dQ, dK, dV as with the saved mask."""
+    from fa2_triton_amd import flash_attn_func, wrapper
+
+    q, k, v, do = generate_test_data(2, 4, 2, 300, 300, 128, torch.bfloat16)
+    out = flash_attn_func(q, k, v, None, None, 0.15, True, None, 777)
+    g_mask = torch.autograd.grad(out, (q, k, v), do)
+    real_empty = torch.empty
+
+    def empty_oom(*a, **kw):
+        if kw.get("dtype") is torch.int32:
+            raise torch.OutOfMemoryError("forced")
+        return real_empty(*a, **kw)
+
+    monkeypatch.setattr(wrapper.torch, "empty", empty_oom)
+    out2 = flash_attn_func(q, k, v, None, None, 0.15, True, None, 777)
+    monkeypatch.undo()
+    g_regen = torch.autograd.grad(out2, (q, k, v), do)
+    assert torch.equal(out, out2)
+    for a, b_ in zip(g_mask, g_regen):
+        assert torch.equal(a, b_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_varlen_dropout_saved_mask(causal):
+    """Dropout with a right-padded attention_mask (varlen, cu_seqlens): the saved keep bits equal
+    Philox at the reference's packed offsets (kernel.py:146-148 with cu_seqlens) on every visible
+    element of every sequence, and a backward reading them is bitwise equal to one regenerating
+    them (this combination was unpinned)."""
+    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from fa2_triton_amd.utils import dropout_mask_words
+    from oracle.philox import rand_torch
+
+    b, hq, hkv, s, d, p = 3, 4, 2, 300, 128, 0.2
+    q, k, v, do = generate_test_data(b, hq, hkv, s, s, d, torch.bfloat16)
+    lens = [300, 173, 1]
+    mask = torch.zeros(b, s, dtype=torch.bool, device=q.device)
+    for i, n in enumerate(lens):
+        mask[i, :n] = True
+    seed = 99
+    words = torch.full((dropout_mask_words(b, hq, s, s),), -1, dtype=torch.int32, device=q.device)
+    o, lse, scale, seed = _flash_attn_forward(q, k, v, mask, None, p, causal, None, seed, dropout_mask=words)
+    keep = _unpack_keep_mask(words, b, hq, s, s)
+    cu = 0
+    for i, n in enumerate(lens):
+        rows = torch.arange(n, device=q.device)
+        for h in range(hq):
+            # packed offset of (row, key) of sequence i, head h: Lk (cu + Lq h) + Lq... as the forward
+            off = n * (cu + n * h) + rows[:, None] * n + rows[None, :]
+            want = rand_torch(seed, off) > p
+            vis = torch.ones(n, n, dtype=torch.bool, device=q.device)
+            if causal:
+                vis = rows[None, :] <= rows[:, None]
+            assert torch.equal(keep[i, h, :n, :n][vis], want[vis]), (i, h)
+        cu += n
+    g_mask = _flash_attn_backward(do, q, k, v, None, mask, o, lse, p, causal, scale, seed, dropout_mask=words)
+    g_regen = _flash_attn_backward(do, q, k, v, None, mask, o, lse, p, causal, scale, seed)
+    for x, y in zip(g_mask, g_regen):
+        if x is not None:
+            assert torch.equal(x, y)

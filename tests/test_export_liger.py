@@ -48,3 +48,22 @@ def test_export_never_deletes_foreign_files(tmp_path):
     (dst / "wrapper.py").write_text("stale\n")
     subprocess.run([sys.executable, script, str(tmp_path), "--no-lib"], check=True, capture_output=True)
     assert (dst / "mine.py").exists() and (dst / "wrapper.py").read_text() != "stale\n"
+
+
+def test_export_manifest_cannot_reach_outside_or_adopt_foreign_files(tmp_path):
+    """manifest entries that leave the export directory ('..', absolute paths) are
+    ignored on refresh, and a --force export does not adopt the foreign files it overwrote (so a
+    later refresh does not delete them)."""
+    script = os.path.join(ROOT, "scripts", "export_to_liger.py")
+    dst = tmp_path / "src" / "liger_kernel" / "ops" / "flash_attention"
+    dst.mkdir(parents=True)
+    (dst / "utils.py").write_text("foreign = True\n")  # same name as a package file
+    subprocess.run([sys.executable, script, str(tmp_path), "--no-lib", "--force"], check=True, capture_output=True)
+    manifest = (dst / ".fa2_export_manifest").read_text().split()
+    assert "utils.py" not in manifest and "wrapper.py" in manifest
+    outside = tmp_path / "outside.txt"
+    outside.write_text("keep\n")
+    (dst / ".fa2_export_manifest").write_text("\n".join(manifest + ["../../../../outside.txt", str(outside)]) + "\n")
+    subprocess.run([sys.executable, script, str(tmp_path), "--no-lib"], check=True, capture_output=True)
+    assert outside.read_text() == "keep\n"
+    assert (dst / "utils.py").exists()
