@@ -7,6 +7,8 @@ forward + one backward of that batch.  The other BASELINE configs have presets t
   --config cfg2   B=8 H=16 S=1024 D=64 bf16 non-causal, forward only (configs[1]);
   --config cfg5   B=2 Hq=32 Hkv=8 S=8192 D=128 fp16 causal fwd+bwd (configs[4]; B=2 assumed,
                   SURVEY.md section 8.0);
+  --config refbench  B=4 H=32 S=4096 D=128 fp16 non-causal forward only (the reference's own
+                  benchmarks/targetted_bench.py shape);
 and every field can be overridden (--batch --heads --heads-kv --seqlen --head-dim --dtype
 --no-causal --fwd-only).  `--bias` adds the reference tests' additive bias (a [1, 1, Sq, Sk]
 tensor in the input dtype, /root/reference/tests/core.py:28) and `--dropout P` dropout with a
@@ -66,6 +68,9 @@ CONFIGS = {
                  ref="BASELINE.json configs[2]; configs[3] = B=64 batch-sharded over 8 GPUs"),
     "cfg5": dict(batch=2, heads=32, heads_kv=8, seqlen=8192, head_dim=128, dtype="fp16", causal=True, fwd_only=False,
                  ref="BASELINE.json configs[4], B=2 assumed (SURVEY.md section 8.0)"),
+    # the reference's own benchmark shape (/root/reference/benchmarks/targetted_bench.py:11-19)
+    "refbench": dict(batch=4, heads=32, heads_kv=32, seqlen=4096, head_dim=128, dtype="fp16", causal=False,
+                     fwd_only=True, ref="the reference's benchmarks/targetted_bench.py shape (fp16, non-causal, fwd)"),
 }
 DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16}
 DROPOUT_SEED = 20241008
@@ -248,6 +253,8 @@ def cpu_baseline(h, hkv, s, d, causal, fwd_only=False, budget_s=20.0):
         "value": flops / dt / 1e12,
         "unit": "TFLOP/s",
         "cores": threads,
+        "cores_note": "torch threads = every CPU in this process's affinity, capped by OMP_NUM_THREADS when set "
+                      "(the GPU box sets it to its per-GPU CPU share, 16, and asks workloads to stay within it)",
         "kind": "port",
         "sample": f"oracle fp32 {'fwd' if fwd_only else 'fwd+bwd'} (oracle/reference.py), B=1 Hq={heads} "
                   f"Hkv={heads // group} S={s} D={d} causal={causal} (slice of the workload), mean of {reps} reps, "
@@ -419,7 +426,8 @@ def main():
     # ---- per-launch timing with HIP events on the launch stream ---------------------------
     # fwd: one launch; bwd: dQ (recomputes S, dP; also writes delta), then dK/dV, each timed
     # alone through fa2_bwd_stages with a shared delta workspace.
-    reps = max(5, args.steps)
+    # every launch timed on its own (event pair on the launch stream), median of >= 50
+    reps = max(50, args.steps)
     stream = torch.cuda.current_stream(device)
     with torch.no_grad():
         # with dropout, as in the autograd op: the forward saves its keep bits, the backward reads them
@@ -437,16 +445,19 @@ def main():
                                                            dropout_mask=kmask)}
         if not fwd_only:
             calls.update(dq_kernel=bwd(4), dkdv_kernel=bwd(2))
-        times = {}
+        times, spread = {}, {}
         for name, fn in calls.items():
             fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in ev:
+                e0.record(stream)
                 fn()
-            e1.record(stream)
+                e1.record(stream)
             torch.cuda.synchronize()
-            times[name] = e0.elapsed_time(e1) / reps * 1e-3
+            ts = sorted(e0.elapsed_time(e1) * 1e-3 for e0, e1 in ev)
+            times[name] = ts[len(ts) // 2]
+            spread[name] = {"reps": reps, "mean_ms": round(sum(ts) / len(ts) * 1e3, 4),
+                            "min_ms": round(ts[0] * 1e3, 4), "max_ms": round(ts[-1] * 1e3, 4)}
     t_fwd = times["fwd_kernel"]
     t_bwd = sum(t for n, t in times.items() if n != "fwd_kernel")
     fwd_tf = f_fwd / t_fwd / 1e12
@@ -459,6 +470,8 @@ def main():
     kernels = {
         name: {
             "ms": round(t * 1e3, 4),
+            "timing": "median of per-launch HIP-event times",
+            **spread[name],
             "algorithmic_tflops": round(algo[name] / t / 1e12, 1),
             "executed_mfma_tflops": round(executed[name] / t / 1e12, 1),
         }
@@ -470,8 +483,10 @@ def main():
                                                                        True)
     dominant = max(times, key=lambda n: times[n])
     # device symbols the workload dispatches to (the pipelined forward: aligned D, no bias, no dropout)
-    symbol = {"fwd_kernel": "fwd_pipe_kernel" if plain else "fwd_kernel", "dkdv_kernel": "dkdv_kernel",
-              "dq_kernel": "dq_kernel"}
+    hp_fwd = plain and d == 128 and os.environ.get("FA2_FWD_HP", "1") != "0"
+    hp_dkdv = plain and d == 128 and os.environ.get("FA2_DKDV_HP", "1") != "0"
+    symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if plain else "fwd_kernel"),
+              "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel", "dq_kernel": "dq_kernel"}
     esz = q.element_size()
 
     def roofline(name):

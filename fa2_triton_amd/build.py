@@ -60,7 +60,7 @@ def generated_headers():
         from fa2_triton_amd import hp_gen
     finally:
         sys.path.pop(0)
-    return [hp_gen.write_headers()]
+    return hp_gen.write_headers()
 
 
 def deps_mtime() -> float:

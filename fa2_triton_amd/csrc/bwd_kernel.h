@@ -16,8 +16,12 @@
 // the requested dtype, and padded varlen rows are handled in place (no pack/unpack).
 #include <type_traits>
 
+#include <stdlib.h>
+
 #include "common.h"
 #include "fa2_internal.h"
+#include "dkdv_hp_kernel.h"
+#include "dq_hp_kernel.h"
 
 // Schedule constants (measured; the variants they replaced are recorded in DESIGN.md):
 //  dK/dV: S chain with its Q fragments kDkdvLS MFMAs ahead, then the dP chain with its
@@ -1352,6 +1356,14 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if ((stages & 4) && a.seqlen_q > 0) {
+    if constexpr (DT == 128 && !BIAS && !DROPOUT && ALIGNED) {
+      // hand-placed one-wave-per-SIMD dQ (dq_hp_kernel.h) for D = 128 exactly
+      if (dq_hp_ok(a, true)) {
+        launch_dq_hp<BF16, CAUSAL>(a, st);
+        goto dq_done;
+      }
+    }
+    {
     constexpr int NW = DqCfg<DT>::NW, BM = NW * 32;
     constexpr bool PAIR = CAUSAL;
     const int nmb = (a.seqlen_q + BM - 1) / BM;
@@ -1374,7 +1386,9 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     } else {
       dq(std::integral_constant<int, 1>{});
     }
+    }
   }
+dq_done:
   if ((stages & 8) && BIAS && a.dbias && a.seqlen_q > 0 && a.seqlen_k > 0) {
     const int bb = a.bias_stride[0] != 0 ? a.batch : 1, hb = a.bias_stride[1] != 0 ? a.heads_q : 1;
     const int nkc = ((a.seqlen_k + 63) / 64 + kDbiasChunk - 1) / kDbiasChunk;
@@ -1383,6 +1397,14 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
   }
   if ((stages & 2) && a.seqlen_k > 0) {
     const int ns = dkv_split(a);
+    if constexpr (DT == 128 && !BIAS && !DROPOUT && ALIGNED) {
+      // hand-placed one-wave-per-SIMD dK/dV (dkdv_hp_kernel.h) for D = 128 exactly
+      if (dkdv_hp_ok(a, true)) {
+        launch_dkdv_hp<BF16, CAUSAL>(a, ns, st);
+        launch_dkv_reduce<BF16>(a, ns, st);
+        return hipGetLastError();
+      }
+    }
     dim3 grid(((a.seqlen_k + 127) / 128) * a.batch * a.heads_kv * ns);
     auto dkdv = [&](auto biask_c) {
       constexpr int BK = decltype(biask_c)::value;

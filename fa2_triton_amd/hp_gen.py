@@ -53,11 +53,11 @@ class Emitter:
     tables; the values below carry margin over the gfx950 minima (8-pass XDL result -> vector
     read 12, vector write -> MFMA operand 2, transcendental -> use 1, VALU -> permlane 2)."""
 
-    MFMA_RESULT = 18   # MFMA writes r  -> any non-chain access of r
+    MFMA_RESULT = 14   # MFMA writes r  -> any non-chain access of r (8-pass XDL: 12, +2 margin)
     TO_MFMA = 3        # VALU / accvgpr_write writes r -> MFMA reads r
     TRANS_USE = 2      # v_exp writes r -> vector use
     TO_PERM = 3        # VALU writes r -> v_permlane32_swap reads r
-    MFMA_READ_WAR = 4  # MFMA reads r (A/B) -> something writes r
+    MFMA_READ_WAR = 2  # MFMA reads r (A/B) -> a vector instruction writes r (LDS returns land later)
     MFMA_C_WAR = 18    # MFMA reads r as C -> something writes r
     M0_DMA = 2         # s_* writes m0 -> LDS-DMA
 
@@ -125,7 +125,7 @@ class Emitter:
         for r in writes:
             if kind == "mfma" and chain:
                 break
-            if r in self.rd_ab:
+            if r in self.rd_ab and kind != "ds":
                 need = max(need, self.MFMA_READ_WAR - (self.ws - self.rd_ab[r]))
             if r in self.rd_c:
                 need = max(need, self.MFMA_C_WAR - (self.ws - self.rd_c[r]))
@@ -742,6 +742,696 @@ class FwdGen:
         return e.out
 
 
+
+# ----------------------------------------------------------------------------------------------
+# dK / dV (the backward's dominant kernel): dkdv_hp_kernel (csrc/dkdv_hp_kernel.h)
+#
+# Register map of the statement:
+#   v[0:31]     S[kb] accumulators (start as LSE2 rows), then P = exp2(-acc) in place
+#   v[32:63]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place
+#   v[64:79]    PP[kb][sp] packed P (B operand of dV^T += dO^T P), v[80:95] DSP[kb][sp] packed dS
+#   v[96:111]   row-fragment ring (Q then dO, A operands of S and dP), 4 slots
+#   v[112:135]  V fragment ring (B operands of dP), 6 slots
+#   v[136:151]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
+#   v[152:155]  mask bounds LO[kb], HI[kb] of a masked step
+#   a[0:127]    dV^T[kb][dt], a[128:255] dK^T[kb][dt]
+#   K' = -(softmax_scale log2 e) K fragments: compiler-placed "v" operands %[k0]..%[k15]
+# LDS (bytes from the workgroup's base): Q tile of buffer b at 16384 b, dO tile at 16384 b + 8192
+# (Tile<128, 32>), V rows of wave w at 32768 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of
+# buffer b at 98304 + 256 b (+128).
+def DS(kb, i=None):
+    return rng("v", 16 * kb, 16) if i is None else f"v{16 * kb + i}"
+
+
+def DDP(kb, i=None):
+    return rng("v", 32 + 16 * kb, 16) if i is None else f"v{32 + 16 * kb + i}"
+
+
+def DPP(kb, sp, j=None):
+    base = 64 + (kb * 2 + sp) * 4
+    return rng("v", base, 4) if j is None else f"v{base + j}"
+
+
+def DDSP(kb, sp, j=None):
+    base = 80 + (kb * 2 + sp) * 4
+    return rng("v", base, 4) if j is None else f"v{base + j}"
+
+
+def DRR(n):
+    return rng("v", 96 + 4 * (n % 4), 4)
+
+
+DVF_SLOTS = 6
+
+
+def DVF(n):
+    return rng("v", 112 + 4 * (n % DVF_SLOTS), 4)
+
+
+def DTR(n, half=None):
+    base = 136 + 4 * (n % 4)
+    return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
+
+
+DLO = ["v152", "v153"]
+DHI = ["v154", "v155"]
+DK_NVGPR = 156
+
+
+def DDV(kb, dt):
+    return rng("a", (kb * 4 + dt) * 16, 16)
+
+
+def DDK(kb, dt):
+    return rng("a", 128 + (kb * 4 + dt) * 16, 16)
+
+
+# scalar state of the dK/dV statement
+D_G = "s64"        # q-head index in the group
+D_IDX = "s65"      # step index within the head
+D_CM = "s66"       # first query row of the current tile
+D_PAR = "s67"      # buffer parity of the current step
+D_QD = "s[68:71]"  # descriptors of the next step's Q, dO, LSE2 and delta rows
+D_OD = "s[72:75]"
+D_LD = "s[76:79]"
+D_DD = "s[80:83]"
+D_QP = ("s84", "s85")  # next step's Q tile address, dO tile address
+D_OP = ("s86", "s87")
+D_LC = "s88"       # next step's LSE2 / delta byte offset from the row bases
+D_NM = "s89"       # next step's first query row
+D_LEFT = "s90"     # steps after the current one
+D_NMT = "s91"      # next step's tile index within its head
+D_M0 = "s92"
+D_T = "s93"
+D_EX = "s[94:95]"
+D_MK = ["s[96:97]", "s[98:99]"]
+D_SGPR_CLOBBER = list(range(64, 100))
+
+
+class DkdvGen:
+    """dK / dV: 4 waves x 64 keys (two 32-key blocks kb per wave, one wave per SIMD); per step
+    (32 query rows of one q-head) 64 MFMAs: S[kb] = Q K'^T (16), dP[kb] = dO V^T (16),
+    dV^T[kb] += dO^T P (16), dK^T[kb] += Q^T dS (16); every Q / dO / transposed fragment read from
+    LDS feeds both key blocks.  Same math as the reference's dK/dV loop
+    (/root/reference/src/backward/compute_dkdv.py:42-112) and dkdv_kernel."""
+
+    def __init__(self, bf16, causal):
+        self.bf16, self.causal = bf16, causal
+        self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
+        self.e = Emitter()
+
+    # -- pieces ----------------------------------------------------------------------------------
+    def row_read(self, par, n):
+        """Row fragment n of the step: n < 8 Q k-step n, else dO k-step n - 8 (buffer par)."""
+        ks = n % 8
+        imm = par * 16384 + (8192 if n >= 8 else 0) + (ks >> 1) * 2048
+        base = "%[qb1]" if ks & 1 else "%[qb0]"
+        d = DRR(n)
+        self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
+
+    def v_frag(self, n):
+        """V fragment n = 2 ks + kb (keys 32 kb .. of this wave, k-step ks)."""
+        ks, kb = n >> 1, n & 1
+        imm = (ks >> 1) * 4096 + 32 * kb * 64
+        base = "%[vb1]" if ks & 1 else "%[vb0]"
+        d = DVF(n)
+        self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
+
+    def tr_read(self, par, n, half):
+        """Transposed fragment n (n < 8: dO^T, else Q^T) f = n % 8: sp = f >> 2, dt = f & 3."""
+        f = n % 8
+        sp, dt = f >> 2, f & 3
+        imm = par * 16384 + (0 if n >= 8 else 8192) + dt * 2048 + 16 * sp * 64
+        base = "%[tb]" if half else "%[ta]"
+        d = DTR(n, half)
+        self.e.ds_read(f"ds_read_b64_tr_b16 {d}, {base} offset:{imm}", d)
+
+    def init_read(self, par, what, kb, g4):
+        """LSE2 (what 0) rows into S[kb], -delta (what 1) into dP[kb]: register group g4."""
+        imm = par * 256 + what * 128 + 32 * g4
+        d = rng("v", (0 if what == 0 else 32) + 16 * kb + 4 * g4, 4)
+        self.e.ds_read(f"ds_read_b128 {d}, %[lb] offset:{imm}", d)
+
+    def descriptors(self):
+        """Descriptors of the next step's tiles from the cursors (range 0 when there is none)."""
+        e = self.e
+        t2 = "s94"  # (D_EX, free until the rows' DMA)
+        e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
+        e.salu(f"s_cmp_gt_u32 {D_LEFT}, 0")
+        e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
+        e.salu(f"s_cselect_b32 {t2}, 128, 0")
+        for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
+            e.salu(f"s_mov_b32 s{d}, {p0}")
+            e.salu(f"s_and_b32 s{d + 1}, {p1}, 0xffff")
+            e.salu(f"s_mul_i32 s{d + 2}, {D_T}, {rb}")
+            e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+        for base, d in (("lse", 76), ("dl", 80)):
+            e.salu(f"s_add_u32 s{d}, %[{base}lo], {D_LC}")
+            e.salu(f"s_addc_u32 s{d + 1}, %[{base}hi], 0")
+            e.salu(f"s_and_b32 s{d + 1}, s{d + 1}, 0xffff")
+            e.salu(f"s_mov_b32 s{d + 2}, {t2}")
+            e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+
+    def advance_cursors(self, tag):
+        """Cursors to the step after the next one: one tile down, or the next head's last tile."""
+        e = self.e
+        e.salu(f"s_add_u32 {D_NMT}, {D_NMT}, 1")
+        e.salu(f"s_cmp_eq_u32 {D_NMT}, %[nmt]")
+        e.raw(f"s_cbranch_scc1 .Lhp%=_{tag}_wrap")
+        e.salu(f"s_sub_u32 {D_NM}, {D_NM}, 32")
+        e.salu(f"s_sub_u32 {D_QP[0]}, {D_QP[0]}, %[qtile]")
+        e.salu(f"s_subb_u32 {D_QP[1]}, {D_QP[1]}, 0")
+        e.salu(f"s_sub_u32 {D_OP[0]}, {D_OP[0]}, %[otile]")
+        e.salu(f"s_subb_u32 {D_OP[1]}, {D_OP[1]}, 0")
+        e.salu(f"s_sub_u32 {D_LC}, {D_LC}, 128")
+        e.raw(f"s_branch .Lhp%=_{tag}_adv")
+        e.label(f".Lhp%=_{tag}_wrap")
+        e.salu(f"s_mov_b32 {D_NMT}, 0")
+        e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
+        e.salu(f"s_add_u32 {D_QP[0]}, {D_QP[0]}, %[qwrap]")
+        e.salu(f"s_addc_u32 {D_QP[1]}, {D_QP[1]}, 0")
+        e.salu(f"s_add_u32 {D_OP[0]}, {D_OP[0]}, %[owrap]")
+        e.salu(f"s_addc_u32 {D_OP[1]}, {D_OP[1]}, 0")
+        e.salu(f"s_add_u32 {D_LC}, {D_LC}, %[lwrap]")
+        e.label(f".Lhp%=_{tag}_adv")
+
+    def dma_items(self, par, tag):
+        """The step's DMA pieces (Q, dO of the next step into buffer 1 - par; wave 0 also its
+        LSE2 / delta rows) as (cost, emit) items; m0 is set one item ahead."""
+        nb = 1 - par
+        pieces = [("q", 0), ("q", 1), ("o", 0), ("o", 1)]
+
+        def m0_of(w_, it):
+            return nb * 16384 + (8192 if w_ == "o" else 0) + it * 4096
+
+        out = []
+        for n, (w_, it) in enumerate(pieces):
+            def f(n=n, w_=w_, it=it):
+                if n == 0:
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(w_, it)}", m0=True)
+                off = f"%[{'q' if w_ == 'q' else 'o'}off{it}]"
+                self.e.dma(f"buffer_load_dwordx4 {off}, {D_QD if w_ == 'q' else D_OD}, 0 offen lds")
+                if n + 1 < len(pieces):
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(*pieces[n + 1])}", m0=True)
+            out.append((16, f))
+
+        def rows(tag=tag):
+            e = self.e
+            e.raw("s_cmp_eq_u32 %[w0], 0")
+            e.raw(f"s_cbranch_scc0 .Lhp%=_{tag}_nl")
+            e.salu(f"s_mov_b64 {D_EX}, exec")
+            e.salu("s_mov_b64 exec, 0xff")
+            e.salu(f"s_add_u32 m0, %[lbs], {nb * 256}", m0=True)
+            e.dma(f"buffer_load_dwordx4 %[lsoff], {D_LD}, 0 offen lds")
+            e.salu(f"s_add_u32 m0, %[lbs], {nb * 256 + 128}", m0=True)
+            e.dma(f"buffer_load_dwordx4 %[lsoff], {D_DD}, 0 offen lds")
+            e.salu(f"s_mov_b64 exec, {D_EX}")
+            e.label(f".Lhp%=_{tag}_nl")
+        out.append((16, rows))
+        return out
+
+    def mask_elem(self, kb, i):
+        """P = LO[kb] <= o < HI[kb] ? P : 0 for the register i of key block kb (o = row offset)."""
+        e = self.e
+        o = (i & 3) + 8 * (i >> 2)
+        r = DS(kb, i)
+        ma, mb = D_MK[i & 1], D_MK[(i & 1) ^ 1] if False else D_MK[i & 1]
+        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, {DLO[kb]}, {o}", None, [DLO[kb]])
+        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, {DHI[kb]}, {o}", None, [DHI[kb]])
+        e.salu(f"s_and_b64 {D_MK[0]}, {D_MK[0]}, {D_MK[1]}")
+        e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
+
+    # -- one step --------------------------------------------------------------------------------
+    def step(self, par, cls, tag):
+        e = self.e
+        live = cls in ("A", "B")
+        masked = cls == "B"
+        self.descriptors()
+        dma = self.dma_items(par, tag)
+        if not live:
+            for _, f in dma:
+                f()
+        else:
+            if masked:
+                for kb in range(2):
+                    e.valu(f"v_subrev_u32 {DLO[kb]}, {D_CM}, %[lo{kb}]", DLO[kb], [])
+                    e.valu(f"v_subrev_u32 {DHI[kb]}, {D_CM}, %[hi{kb}]", DHI[kb], [])
+            g = GapScheduler(64)
+            # LSE2 rows into S[kb] (before the first S MFMA), -delta rows into dP[kb]
+            for what in range(2):
+                for kb in range(2):
+                    for g4 in range(4):
+                        rel, dl = (-1, -1) if what == 0 else (-1, 12)
+                        g.add(f"init{what}", 4, rel, dl, lambda what=what, kb=kb, g4=g4: self.init_read(par, what, kb, g4))
+            # row fragments: Q (S phase) then dO (dP phase), 3 ahead; V fragments 3 ahead
+            for n in range(16):
+                mf = 2 * n  # first MFMA using it (S: 2 ks, dP: 16 + 2 ks)
+                rel = -1 if n < 3 else mf - 6
+                g.add("row", 4, rel, max(rel, mf - 4), lambda n=n: self.row_read(par, n))
+            for n in range(16):
+                mf = 16 + n
+                rel = -1 if n < DVF_SLOTS - 1 else mf - DVF_SLOTS + 1
+                g.add("vf", 4, rel, max(rel, mf - 3), lambda n=n: self.v_frag(n))
+            # exponentials (after the S chains), mask, P packs
+            for sp in range(2):
+                for kb in range(2):
+                    for i in range(8 * sp, 8 * sp + 8):
+                        r = DS(kb, i)
+                        g.add(f"exp{kb}", 8, 19, 27 + 8 * sp,
+                              lambda r=r: e.valu(f"v_exp_f32_e64 {r}, -{r}", r, [r], kind="trans"))
+                        if masked:
+                            g.add(f"exp{kb}", 16, 19, 28 + 8 * sp, lambda kb=kb, i=i: self.mask_elem(kb, i))
+                    for j in range(4):
+                        g.add(f"exp{kb}", 4, 19, 29 + 8 * sp,
+                              lambda kb=kb, sp=sp, j=j: self.cvt(DPP(kb, sp, j), DS(kb, 8 * sp + 2 * j), DS(kb, 8 * sp + 2 * j + 1)))
+            # dS = P dP' after the dP chains, dS packs
+            for kb in range(2):
+                for sp in range(2):
+                    for i in range(8 * sp, 8 * sp + 8):
+                        a_, b_ = DS(kb, i), DDP(kb, i)
+                        g.add(f"ds{kb}", 4, 35, 44 + 8 * sp, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
+                    for j in range(4):
+                        g.add(f"ds{kb}", 4, 35, 45 + 8 * sp,
+                              lambda kb=kb, sp=sp, j=j: self.cvt(DDSP(kb, sp, j), DDP(kb, 8 * sp + 2 * j), DDP(kb, 8 * sp + 2 * j + 1)))
+            # transposed fragments: dO^T (dV) then Q^T (dK), 3 ahead
+            for n in range(16):
+                mf = 32 + 2 * n
+                rel = max(0, mf - 6)
+                for h in range(2):
+                    g.add("tr", 4, rel, mf - 3, lambda n=n, h=h: self.tr_read(par, n, h))
+            for n, (c, f) in enumerate(dma):
+                g.add("dma", c, 2, 40 + n, f)
+
+            def mfma(i):
+                if i < 16:  # S[kb] += Q(ks) K'[kb](ks)
+                    ks, kb = i >> 1, i & 1
+                    e.mfma(self.mop, DS(kb), DRR(ks), f"%[k{kb * 8 + ks}]", DS(kb))
+                elif i < 32:  # dP[kb] += dO(ks) V[kb](ks)
+                    ks, kb = (i - 16) >> 1, i & 1
+                    e.mfma(self.mop, DDP(kb), DRR(8 + ks), DVF(2 * ks + kb), DDP(kb))
+                elif i < 48:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
+                    f, kb = (i - 32) >> 1, i & 1
+                    sp, dt = f >> 2, f & 3
+                    e.mfma(self.mop, DDV(kb, dt), DTR(f), DPP(kb, sp), DDV(kb, dt))
+                else:  # dK^T[kb][dt] += Q^T(sp, dt) dS[kb](sp)
+                    f, kb = (i - 48) >> 1, i & 1
+                    sp, dt = f >> 2, f & 3
+                    e.mfma(self.mop, DDK(kb, dt), DTR(8 + f), DDSP(kb, sp), DDK(kb, dt))
+
+            g.run(mfma, pre_budget=48)
+        self.advance_cursors(tag)
+        e.salu(f"s_sub_u32 {D_LEFT}, {D_LEFT}, 1")
+        e.salu(f"s_sub_u32 {D_CM}, {D_CM}, 32")
+        e.salu(f"s_xor_b32 {D_PAR}, {D_PAR}, 1")
+        e.drain_lds()
+        e.raw("s_waitcnt vmcnt(0)")
+        e.raw("s_barrier")
+        e.reset()
+
+    def cvt(self, d, a, b):
+        self.e.valu(f"{self.cvtop} {d}, {a}, {b}", d, [a, b])
+
+    def build(self):
+        e = self.e
+        e.raw("s_nop 7")
+        e.raw("s_nop 7")
+        e.salu(f"s_mov_b32 {D_M0}, m0")
+        for r in range(256):
+            e.valu(f"v_accvgpr_write_b32 a{r}, 0", f"a{r}", kind="accw")
+        # cursors: the step after step 0
+        e.salu(f"s_mov_b32 {D_QP[0]}, %[qlo]")
+        e.salu(f"s_mov_b32 {D_QP[1]}, %[qhi]")
+        e.salu(f"s_mov_b32 {D_OP[0]}, %[olo]")
+        e.salu(f"s_mov_b32 {D_OP[1]}, %[ohi]")
+        e.salu(f"s_mov_b32 {D_LC}, %[lc0]")
+        e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
+        e.salu(f"s_mov_b32 {D_NMT}, 0")
+        self.advance_cursors("init")
+        e.salu(f"s_mov_b32 {D_LEFT}, %[total]")
+        e.salu(f"s_sub_u32 {D_LEFT}, {D_LEFT}, 1")
+        e.salu(f"s_mov_b32 {D_G}, 0")
+        e.salu(f"s_mov_b32 {D_PAR}, 0")
+        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.raw("s_barrier")
+        e.reset()
+        e.raw("s_cmp_eq_u32 %[total], 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_end")
+        # head loop
+        e.label(".Lhp%=_head")
+        e.salu(f"s_mov_b32 {D_IDX}, 0")
+        e.salu(f"s_mov_b32 {D_CM}, %[mlast]")
+        e.raw(".balignl 64, 0xbf800000", 0)
+        e.label(".Lhp%=_step")
+        # class of step IDX: [0, c0) B, [c0, c01) A, [c01, c012) B, then D
+        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c0]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
+        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c01]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsA")
+        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c012]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
+        e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_D0")
+        e.raw("s_branch .Lhp%=_D1")
+        e.label(".Lhp%=_clsA")
+        e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_A1")
+        for cls, par in (("A", 0), ("A", 1), ("B", 0), ("B", 1), ("D", 0), ("D", 1)):
+            if (cls, par) == ("B", 0):
+                e.label(".Lhp%=_clsB")
+                e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
+                e.raw("s_cbranch_scc0 .Lhp%=_B1")
+            e.label(f".Lhp%=_{cls}{par}")
+            self.step(par, cls, f"{cls.lower()}{par}")
+            e.raw("s_branch .Lhp%=_next")
+        e.label(".Lhp%=_next")
+        e.salu(f"s_add_u32 {D_IDX}, {D_IDX}, 1")
+        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[nmt]")
+        e.raw("s_cbranch_scc1 .Lhp%=_step")
+        e.salu(f"s_add_u32 {D_G}, {D_G}, 1")
+        e.raw(f"s_cmp_lt_u32 {D_G}, %[ng]")
+        e.raw("s_cbranch_scc1 .Lhp%=_head")
+        e.label(".Lhp%=_end")
+        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.salu(f"s_mov_b32 m0, {D_M0}")
+        e.raw("s_nop 15")
+        e.raw("s_nop 15")
+        return e.out
+
+
+def gen_dkdv_function(bf16, causal):
+    g = DkdvGen(bf16, causal)
+    lines = g.build()
+    name = f"dkdv_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    clob = [f'"v{i}"' for i in range(DK_NVGPR)] + [f'"a{i}"' for i in range(256)] + \
+           [f'"s{i}"' for i in D_SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
+    kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
+    sops = ["ng", "nmt", "total", "c0", "c01", "c012", "mlast", "lq", "qrb", "orb", "qtile", "otile", "qwrap",
+            "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0"]
+    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1", "ooff0", "ooff1", "lsoff",
+            "lo0", "lo1", "hi0", "hi1"]
+    src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
+  asm volatile(
+{_asm_body(lines)}
+      :
+      : {kops},
+        {", ".join(f'[{n}] "v"(a.{n})' for n in vops)},
+        {", ".join(f'[{n}] "s"(a.{n})' for n in sops)}
+      : {", ".join(clob)});
+}}
+"""
+    return src
+
+
+def gen_read_dkdv():
+    parts = ["// dV^T a[0:127], dK^T a[128:255] -> registers (after the statement's final drain)",
+             "FA2_DEV void dkdv_hp_read(f32x16 (&dv)[2][4], f32x16 (&dk)[2][4]) {"]
+    for which, base0 in (("dv", 0), ("dk", 128)):
+        for kb in range(2):
+            for dt in range(4):
+                base = base0 + (kb * 4 + dt) * 16
+                outs = ", ".join(f'"=v"({which}[{kb}][{dt}][{i}])' for i in range(16))
+                body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
+                parts.append(f'  asm volatile("{body}" : {outs});')
+    parts.append("}")
+    return "\n".join(parts) + "\n"
+
+
+
+# ----------------------------------------------------------------------------------------------
+# dQ: dq_hp_kernel (csrc/dq_hp_kernel.h)
+#
+# Register map of the statement:
+#   v[0:63]     S^T[rb][h] (scores of key half h; then P), v[64:127] dP^T[rb][h] (then dS)
+#   v[128:159]  DSP[rb][kk] packed dS^T (B operand of dQ^T += K^T dS^T)
+#   v[160:175]  K row-fragment ring, v[176:191] V row-fragment ring, v[192:207] K^T ring
+#   v[208:209]  mask limits of a masked tile
+#   a[0:127]    dQ^T[rb][dt]; a[128:255] the Q' (= scale log2 e Q) and dO fragments ("a" operands)
+def QS(rb, h, i=None):
+    base = (rb * 2 + h) * 16
+    return rng("v", base, 16) if i is None else f"v{base + i}"
+
+
+def QDP(rb, h, i=None):
+    base = 64 + (rb * 2 + h) * 16
+    return rng("v", base, 16) if i is None else f"v{base + i}"
+
+
+def QDSP(rb, kk, j=None):
+    base = 128 + (rb * 4 + kk) * 4
+    return rng("v", base, 4) if j is None else f"v{base + j}"
+
+
+def QKR(n):
+    return rng("v", 160 + 4 * (n % 4), 4)
+
+
+def QVR(n):
+    return rng("v", 176 + 4 * (n % 4), 4)
+
+
+def QTR(n, half=None):
+    base = 192 + 4 * (n % 4)
+    return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
+
+
+QREL = ["v208", "v209"]
+DQ_NVGPR = 210
+
+
+def QDQ(rb, dt):
+    return rng("a", (rb * 4 + dt) * 16, 16)
+
+
+# scalar state of the dQ statement (shares the forward's cursor registers)
+Q_SN0 = "s66"  # first key of the current tile
+
+
+class DqGen:
+    """dQ (recompute form, deterministic): 4 waves x 64 query rows (two 32-row blocks rb per
+    wave, one wave per SIMD); per 64-key tile 96 MFMAs: S^T = K Q'^T (32), dP^T = V dO^T (32),
+    dQ^T += K^T dS^T (32); every K, V and K^T fragment read from LDS feeds both row blocks.
+    Same math as the reference's dQ loop (/root/reference/src/backward/compute_dq.py:38-78)
+    and dq_kernel: P = exp2(s scale log2 e - LSE2), dS = P (dP - delta), dQ = scale dS K."""
+
+    def __init__(self, bf16, causal):
+        self.bf16, self.causal = bf16, causal
+        self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
+        self.e = Emitter()
+
+    def k_read(self, par, n):
+        h, ks = n // 8, n % 8
+        imm = par * 16384 + (ks >> 1) * 4096 + 32 * h * 64
+        d = QKR(n)
+        self.e.ds_read(f"ds_read_b128 {d}, {'%[kb1]' if ks & 1 else '%[kb0]'} offset:{imm}", d)
+
+    def v_read(self, par, n):
+        h, ks = n // 8, n % 8
+        imm = 32768 + par * 16384 + (ks >> 1) * 4096 + 32 * h * 64
+        d = QVR(n)
+        self.e.ds_read(f"ds_read_b128 {d}, {'%[kb1]' if ks & 1 else '%[kb0]'} offset:{imm}", d)
+
+    def t_read(self, par, n, half):
+        kk, dt = n // 4, n % 4
+        imm = par * 16384 + dt * 4096 + 16 * kk * 64
+        d = QTR(n, half)
+        self.e.ds_read(f"ds_read_b64_tr_b16 {d}, {'%[tb]' if half else '%[ta]'} offset:{imm}", d)
+
+    def descriptors(self):
+        FwdGen.descriptors(self)
+
+    def dma_items(self, par):
+        """K(i+1), V(i+1) into buffer 1 - par (m0 one item ahead)."""
+        nb = 1 - par
+        pieces = [("k", it) for it in range(4)] + [("v", it) for it in range(4)]
+
+        def m0_of(w_, it):
+            return nb * 16384 + it * 4096 + (32768 if w_ == "v" else 0)
+
+        out = []
+        for n, (w_, it) in enumerate(pieces):
+            def f(n=n, w_=w_, it=it):
+                if n == 0:
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(w_, it)}", m0=True)
+                self.e.dma(f"buffer_load_dwordx4 %[off{it}], {SKD if w_ == 'k' else SVD}, 0 offen lds")
+                if n + 1 < len(pieces):
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(*pieces[n + 1])}", m0=True)
+            out.append((16, f))
+        return out
+
+    def mask_elem(self, rb, h, i):
+        """P = key offset o < REL[rb] ? P : 0 (o = 32 h + (i & 3) + 8 (i >> 2))."""
+        e = self.e
+        o = 32 * h + (i & 3) + 8 * (i >> 2)
+        r = QS(rb, h, i)
+        sm = SMASK[i & 1]
+        e.valu(f"v_cmp_gt_i32_e64 {sm}, {QREL[rb]}, {o}", None, [QREL[rb]])
+        e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {sm}", r, [r])
+
+    def cvt(self, d, a, b):
+        self.e.valu(f"{self.cvtop} {d}, {a}, {b}", d, [a, b])
+
+    def period(self, par, cls):
+        e = self.e
+        self.descriptors()
+        dma = self.dma_items(par)
+        if cls == "D":
+            for _, f in dma:
+                f()
+        else:
+            masked = cls == "B"
+            if masked:
+                for rb in range(2):
+                    e.valu(f"v_subrev_u32 {QREL[rb]}, {Q_SN0}, %[rel{rb}]", QREL[rb], [])
+            g = GapScheduler(96)
+            for n in range(16):  # K row fragments, then V row fragments: 3 ahead (ring of 4)
+                mf = 2 * n
+                rel = -1 if n < 3 else mf - 6
+                g.add("k", 4, rel, max(rel, mf - 4), lambda n=n: self.k_read(par, n))
+            for n in range(16):
+                mf = 32 + 2 * n
+                rel = max(-1, mf - 6)
+                g.add("v", 4, rel, mf - 4, lambda n=n: self.v_read(par, n))
+            for n in range(16):  # K^T fragments for dQ: 3 ahead
+                mf = 64 + 2 * n
+                for hf in range(2):
+                    g.add("t", 4, mf - 6, mf - 3, lambda n=n, hf=hf: self.t_read(par, n, hf))
+            for h in range(2):
+                rel0 = 18 + 16 * h
+                for rb in range(2):
+                    for i in range(16):
+                        r = QS(rb, h, i)
+                        st = f"p{h}{rb}"
+                        g.add(st, 4, rel0, 38 + 16 * h,
+                              lambda r=r, rb=rb: e.valu(f"v_sub_f32 {r}, {r}, %[lse{rb}]", r, [r]))
+                        g.add(st, 8, rel0, 40 + 16 * h, lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
+                        if masked:
+                            g.add(st, 8, rel0, 41 + 16 * h, lambda rb=rb, h=h, i=i: self.mask_elem(rb, h, i))
+                rel1 = 50 + 16 * h
+                for rb in range(2):
+                    for i in range(16):
+                        a_, b_ = QS(rb, h, i), QDP(rb, h, i)
+                        st = f"d{h}{rb}"
+                        g.add(st, 4, rel1, 58 + 16 * h,
+                              lambda b_=b_, rb=rb: e.valu(f"v_sub_f32 {b_}, {b_}, %[del{rb}]", b_, [b_]))
+                        g.add(st, 4, rel1, 60 + 16 * h, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
+                        if i & 1:
+                            kk, j = 2 * h + (i >> 3), (i & 7) >> 1
+                            g.add(st, 4, rel1, 62 + 16 * h,
+                                  lambda rb=rb, kk=kk, j=j, h=h, i=i: self.cvt(QDSP(rb, kk, j), QDP(rb, h, i - 1), QDP(rb, h, i)))
+            for n, (c, f) in enumerate(dma):
+                g.add("dma", c, 0, 40 + 4 * n, f)
+
+            def mfma(gi):
+                if gi < 32:
+                    h, ks, rb = gi >> 4, (gi >> 1) & 7, gi & 1
+                    d = QS(rb, h)
+                    e.mfma(self.mop, d, QKR(8 * h + ks), f"%[q{rb * 8 + ks}]", "0" if ks == 0 else d)
+                elif gi < 64:
+                    x = gi - 32
+                    h, ks, rb = x >> 4, (x >> 1) & 7, x & 1
+                    d = QDP(rb, h)
+                    e.mfma(self.mop, d, QVR(8 * h + ks), f"%[o{rb * 8 + ks}]", "0" if ks == 0 else d)
+                else:
+                    f_, rb = (gi - 64) >> 1, gi & 1
+                    kk, dt = f_ >> 2, f_ & 3
+                    e.mfma(self.mop, QDQ(rb, dt), QTR(f_), QDSP(rb, kk), QDQ(rb, dt))
+
+            g.run(mfma, pre_budget=48)
+        e.salu(f"s_add_i32 {SI}, {SI}, 1")
+        e.salu(f"s_add_i32 {Q_SN0}, {Q_SN0}, 64")
+        e.drain_lds()
+        e.raw("s_waitcnt vmcnt(0)")
+        e.raw("s_barrier")
+        e.reset()
+
+    def build(self):
+        e = self.e
+        e.raw("s_nop 7")
+        e.raw("s_nop 7")
+        e.salu(f"s_mov_b32 {SM0}, m0")
+        for r in range(128):
+            e.valu(f"v_accvgpr_write_b32 a{r}, 0", f"a{r}", kind="accw")
+        # DMA cursors: period i requests K(i + 1), V(i + 1)
+        e.salu(f"s_mov_b32 {SKP[0]}, %[klo]")
+        e.salu(f"s_mov_b32 {SKP[1]}, %[khi]")
+        e.salu(f"s_mov_b32 {SVP[0]}, %[vlo]")
+        e.salu(f"s_mov_b32 {SVP[1]}, %[vhi]")
+        e.salu(f"s_mov_b32 {SKR}, %[kbytes]")
+        e.salu(f"s_mov_b32 {SVR}, %[kbytes]")
+        for p0, p1, rem in ((SKP[0], SKP[1], SKR), (SVP[0], SVP[1], SVR)):
+            e.salu(f"s_add_u32 {p0}, {p0}, %[tileb]")
+            e.salu(f"s_addc_u32 {p1}, {p1}, 0")
+            e.salu(f"s_sub_i32 {rem}, {rem}, %[tileb]")
+        e.salu(f"s_mov_b32 {SI}, 0")
+        e.salu(f"s_mov_b32 {Q_SN0}, 0")
+        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.raw("s_barrier")
+        e.reset()
+        e.raw(".balignl 64, 0xbf800000", 0)
+        e.label(".Lhp%=_A")
+        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_B")
+        self.period(0, "A")
+        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_B")
+        self.period(1, "A")
+        e.raw("s_branch .Lhp%=_A")
+        e.label(".Lhp%=_B")
+        e.raw(f"s_cmp_gt_i32 {SI}, %[last]")
+        e.raw("s_cbranch_scc1 .Lhp%=_D")
+        e.raw(f"s_bitcmp1_b32 {SI}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_B1")
+        self.period(0, "B")
+        e.raw("s_branch .Lhp%=_B")
+        e.label(".Lhp%=_B1")
+        self.period(1, "B")
+        e.raw("s_branch .Lhp%=_B")
+        e.label(".Lhp%=_D")
+        e.raw(f"s_cmp_ge_i32 {SI}, %[ntiles]")
+        e.raw("s_cbranch_scc1 .Lhp%=_end")
+        e.raw(f"s_bitcmp1_b32 {SI}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_D1")
+        self.period(0, "D")
+        e.raw("s_branch .Lhp%=_D")
+        e.label(".Lhp%=_D1")
+        self.period(1, "D")
+        e.raw("s_branch .Lhp%=_D")
+        e.label(".Lhp%=_end")
+        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.salu(f"s_mov_b32 m0, {SM0}")
+        e.raw("s_nop 15")
+        e.raw("s_nop 15")
+        return e.out
+
+
+def gen_dq_function(bf16, causal):
+    g = DqGen(bf16, causal)
+    lines = g.build()
+    name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    clob = [f'"v{i}"' for i in range(DQ_NVGPR)] + [f'"a{i}"' for i in range(128)] + \
+           [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
+    qops = ", ".join(f'[q{i}] "a"(q[{i}])' for i in range(16))
+    oops = ", ".join(f'[o{i}] "a"(o[{i}])' for i in range(16))
+    vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1"]
+    sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi"]
+    src = f"""// hand-placed dQ statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+FA2_DEV void {name}(const u32x4 (&q)[16], const u32x4 (&o)[16], const DqHpArgs& a) {{
+  asm volatile(
+{_asm_body(lines)}
+      :
+      : {qops},
+        {oops},
+        {", ".join(f'[{n}] "v"(a.{n})' for n in vops)},
+        {", ".join(f'[{n}] "s"(a.{n})' for n in sops)}
+      : {", ".join(clob)});
+}}
+"""
+    return src
+
+
 def _asm_body(lines):
     return "\n".join(f'      "{l}\\n"' for l in lines)
 
@@ -793,7 +1483,25 @@ def write_headers():
     out.append(gen_read_o())
     out.append("}  // namespace fa2\n")
     text = "\n".join(out)
-    path = os.path.join(GEN, "fwd_hp_body.h")
+    paths = [_write(os.path.join(GEN, "fwd_hp_body.h"), text)]
+    out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
+    for bf16 in (True, False):
+        for causal in (True, False):
+            out.append(gen_dkdv_function(bf16, causal))
+    out.append(gen_read_dkdv())
+    out.append("}  // namespace fa2\n")
+    paths.append(_write(os.path.join(GEN, "dkdv_hp_body.h"), "\n".join(out)))
+    out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
+    for bf16 in (True, False):
+        for causal in (True, False):
+            out.append(gen_dq_function(bf16, causal))
+    out.append(gen_read_o().replace("fwd_hp_read_o", "dq_hp_read").replace("O^T accumulators", "dQ^T accumulators"))
+    out.append("}  // namespace fa2\n")
+    paths.append(_write(os.path.join(GEN, "dq_hp_body.h"), "\n".join(out)))
+    return paths
+
+
+def _write(path, text):
     if not os.path.exists(path) or open(path).read() != text:
         with open(path, "w") as f:
             f.write(text)

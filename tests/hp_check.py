@@ -52,6 +52,63 @@ def run(case):
     return ok
 
 
+BWD_CASES = [
+    # b, hq, hkv, sq, sk, causal, dtype
+    (1, 1, 1, 256, 256, False, torch.bfloat16),
+    (1, 1, 1, 256, 256, True, torch.bfloat16),
+    (2, 4, 2, 512, 512, True, torch.bfloat16),
+    (2, 4, 4, 1024, 1024, False, torch.float16),
+    (1, 2, 1, 300, 700, True, torch.bfloat16),
+    (1, 2, 2, 777, 333, True, torch.float16),
+    (1, 4, 1, 129, 257, False, torch.bfloat16),
+    (2, 8, 8, 2048, 2048, True, torch.bfloat16),
+]
+
+
+def run_bwd(case):
+    from fa2_triton_amd.backward import _flash_attn_backward
+
+    b, hq, hkv, sq, sk, causal, dt = case
+    torch.manual_seed(1)
+    q = (torch.randn(b, sq, hq, 128, device="cuda", dtype=dt) * 0.5).requires_grad_()
+    k = (torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5).requires_grad_()
+    v = (torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5).requires_grad_()
+    do = torch.randn(b, sq, hq, 128, device="cuda", dtype=dt)
+    os.environ["FA2_FWD_HP"] = "0"
+    o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+    res = {}
+    for hp in ("1", "0"):
+        os.environ["FA2_DKDV_HP"] = hp
+        os.environ["FA2_DQ_HP"] = hp
+        g = _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None)
+        torch.cuda.synchronize()
+        res[hp] = [x.float() for x in g[:3]]
+    os.environ.pop("FA2_DKDV_HP")
+    os.environ.pop("FA2_DQ_HP")
+    os.environ.pop("FA2_FWD_HP")
+    ref = attention_reference(q, k, v, causal=causal)
+    gref = torch.autograd.grad(ref, (q, k, v), do.float())
+    pt = attention_reference(q, k, v, causal=causal, upcast=False, reorder_ops=True)
+    gpt = torch.autograd.grad(pt, (q, k, v), do)
+    ok = True
+    msg = []
+    for name, i in (("dQ", 0), ("dK", 1), ("dV", 2)):
+        d = (res["1"][i] - res["0"][i]).abs().max().item()
+        e1 = (res["1"][i] - gref[i].float()).abs().max().item()
+        e0 = (res["0"][i] - gref[i].float()).abs().max().item()
+        ept = (gpt[i].float() - gref[i].float()).abs().max().item()
+        good = e1 <= 3 * ept + 1e-5 and bool(torch.isfinite(res["1"][i]).all())
+        ok &= good
+        msg.append(f"{name}: hp-old {d:.3e} err hp {e1:.3e} old {e0:.3e} pt {ept:.3e}")
+    print(f"bwd {case}: " + " | ".join(msg) + f" {'OK' if ok else 'FAIL'}", flush=True)
+    return ok
+
+
 if __name__ == "__main__":
-    bad = [c for c in CASES if not run(c)]
+    which = sys.argv[1] if len(sys.argv) > 1 else "fwd,bwd"
+    bad = []
+    if "fwd" in which:
+        bad += [c for c in CASES if not run(c)]
+    if "bwd" in which:
+        bad += [c for c in BWD_CASES if not run_bwd(c)]
     sys.exit(1 if bad else 0)

@@ -84,13 +84,13 @@ def test_kernels_match_golden(name, dtype):
     err = (out.float() - ref_out).abs().max().item()
     err_pt = (pt.float() - ref_out).abs().max().item()
     assert err <= 2 * err_pt + 5e-5, (err, err_pt)
-    if True:  # with dropout too: the backward regenerates the forward's keep mask
-        grads = torch.autograd.grad(out, (q, k, v), do)
-        grads_pt = torch.autograd.grad(pt, (q, k, v), do)
-        for nm, gg, gp in zip(("dq", "dk", "dv"), grads, grads_pt):
-            ref = torch.from_numpy(g[nm]).to(dev)
-            e, ep = (gg.float() - ref).abs().max().item(), (gp.float() - ref).abs().max().item()
-            assert e <= 3 * ep + 1e-5, (nm, e, ep)
+    # gradients, with dropout too: the backward regenerates the forward's keep mask
+    grads = torch.autograd.grad(out, (q, k, v), do)
+    grads_pt = torch.autograd.grad(pt, (q, k, v), do)
+    for nm, gg, gp in zip(("dq", "dk", "dv"), grads, grads_pt):
+        ref = torch.from_numpy(g[nm]).to(dev)
+        e, ep = (gg.float() - ref).abs().max().item(), (gp.float() - ref).abs().max().item()
+        assert e <= 3 * ep + 1e-5, (nm, e, ep)
     # LSE2 (base-2 logsumexp) from the forward launcher itself
     with torch.no_grad():
         _, lse, _, _ = fwd_mod._flash_attn_forward(q, k, v, pad, bias, 0.0, m["causal"], None, None)

@@ -63,7 +63,8 @@ def test_shard_batch_covers_uneven_batches():
 
 def _bench_dry_run(*extra):
     """`python bench.py --gpus 2 --dry-run ...` exactly as a user runs it: the script launches
-    its own 2 rank processes (gloo here, RCCL on the GPU box) and rank 0 prints one line."""
+    its own 2 rank processes (host-side gloo coordination, here as on the GPU box: RCCL is never
+    initialised, the data path has no collective) and rank 0 prints one line."""
     import json
     import subprocess
     import sys
