@@ -90,9 +90,10 @@ class Emitter:
                 hit = j
         if hit >= 0:
             n = len(self.ds) - 1 - hit
-            assert n <= 15
-            self._line(f"s_waitcnt lgkmcnt({n})")
-            self.ds = self.ds[hit + 1:]
+            # the counter holds at most 15: waiting for <= 15 outstanding covers every older read
+            # (LDS reads complete in order)
+            self._line(f"s_waitcnt lgkmcnt({min(n, 15)})")
+            self.ds = self.ds[hit + 1:] if n <= 15 else self.ds[-15:]
 
     def _pad(self, need):
         need = max(need, 0)
@@ -343,11 +344,21 @@ class GapScheduler:
 
 
 class FwdGen:
-    def __init__(self, bf16, causal):
-        self.bf16, self.causal = bf16, causal
+    """exact=True: Q enters unscaled and every score gets z = s (scale log2 e) - m_ref in fp32
+    (one v_fma_f32, in the PV phase beside the row max), as the reference scales qk in fp32.
+    exact=False: Q pre-scaled by scale log2 e and rounded to the input dtype, the S chain seeded
+    with -m_ref, so the chain yields z directly (no per-score VALU; costs one extra rounding of
+    the scores, ~2^-9 relative in bf16)."""
+
+    def __init__(self, bf16, causal, exact=True):
+        self.bf16, self.causal, self.exact = bf16, causal, exact
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
+
+    def chain0(self, rb):
+        """Initial accumulator of an S chain: 0 (exact) or INIT = -m_ref (pre-scaled Q)."""
+        return "0" if self.exact else INIT(rb)
 
     # -- pieces ------------------------------------------------------------------------------
     def k_read(self, kbuf, m):
@@ -425,8 +436,27 @@ class FwdGen:
         ops.append((f"v_max_f32 {m}, {m}, {v[15]}", m, [m, v[15]]))
         return ops
 
+    def fma_z(self, st, rb, t, i):
+        """exact: z = s (scale log2 e) - m_ref in place (-m_ref kept in INIT(rb, 0))."""
+        r = S(st, rb, t, i)
+        self.e.valu(f"v_fma_f32 {r}, {r}, %[uz], {INIT(rb, 0)}", r, [r, INIT(rb, 0)])
+
+    def max_ops_z(self, st, rb, t):
+        """The row-max chain of (rb, t); in exact mode each value's fma right after the max op
+        that read it."""
+        out = []
+        ops = self.max_ops(st, rb, t)
+        covered = [[0, 1, 2]] + [[k, k + 1] for k in range(3, 15, 2)] + [[15]]
+        for op, els in zip(ops, covered):
+            out.append(("max",) + op)
+            if self.exact:
+                for i in els:
+                    out.append(("fma", rb, t, i))
+        return out
+
     def row_max_finish(self):
-        """mx[rb] = max over the lane pair of max(MAH[rb][0], MAH[rb][1])."""
+        """mx[rb] = max over the lane pair of max(MAH[rb][0], MAH[rb][1]) (exact: converted to the
+        exponent-argument domain, mx s scale log2 e - m_ref)."""
         e = self.e
         for rb in range(2):
             e.valu(f"v_max_f32 {MX[rb]}, {MAH[rb][0]}, {MAH[rb][1]}", MX[rb], MAH[rb])
@@ -435,6 +465,9 @@ class FwdGen:
             e.valu(f"v_permlane32_swap_b32 {MX[rb]}, {TMP[rb]}", [MX[rb], TMP[rb]], [MX[rb], TMP[rb]], kind="perm")
         for rb in range(2):
             e.valu(f"v_max_f32 {MX[rb]}, {MX[rb]}, {TMP[rb]}", MX[rb], [MX[rb], TMP[rb]])
+        if self.exact:
+            for rb in range(2):
+                e.valu(f"v_fma_f32 {MX[rb]}, {MX[rb]}, %[uz], {INIT(rb, 0)}", MX[rb], [MX[rb], INIT(rb, 0)])
 
     def rescale(self, st, lbl_skip=None):
         """Defer-max rescale: for each row block, m_new = max(m_run, mx + m_ref), m_use = m_new or
@@ -473,8 +506,9 @@ class FwdGen:
             e.valu(f"v_sub_f32 {THR[rb]}, {t_new}, {t_use}", THR[rb], [t_new, t_use])
             e.valu(f"v_add_f32_e32 {THR[rb]}, 0x41000000, {THR[rb]}", THR[rb], [THR[rb]])
             e.valu(f"v_sub_f32 {INIT(rb, 0)}, 0, {t_use}", INIT(rb, 0), [t_use])
-            for j in range(1, 16):
-                e.valu(f"v_mov_b32 {INIT(rb, j)}, {INIT(rb, 0)}", INIT(rb, j), [INIT(rb, 0)])
+            if not self.exact:
+                for j in range(1, 16):
+                    e.valu(f"v_mov_b32 {INIT(rb, j)}, {INIT(rb, 0)}", INIT(rb, j), [INIT(rb, 0)])
 
     def vote_and_rescale(self, st, tag):
         """One wave vote: any row of either block whose max outgrew its threshold -> rescale."""
@@ -505,7 +539,7 @@ class FwdGen:
             t, ks = m // 8, m % 8
             for rb in range(2):
                 d = S(st, rb, t)
-                e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", INIT(rb) if ks == 0 else d)
+                e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", self.chain0(rb) if ks == 0 else d)
 
     def max_mask_plain(self, st, masked):
         """Mask (masked tiles) and row max of set st, no MFMA cover (prologue)."""
@@ -518,8 +552,11 @@ class FwdGen:
                 if masked:
                     for i in range(16):
                         self.mask_elem(st, rb, t, i)
-                for (txt, d, srcs) in self.max_ops(st, rb, t):
-                    e.valu(txt, d, srcs)
+                for op in self.max_ops_z(st, rb, t):
+                    if op[0] == "max":
+                        e.valu(op[1], op[2], op[3])
+                    else:
+                        self.fma_z(st, *op[1:])
         self.row_max_finish()
 
     def period_xy(self, par, cls, tag):
@@ -560,7 +597,7 @@ class FwdGen:
             m, rb = g >> 1, g & 1
             t, ks = m // 8, m % 8
             d = S(nxt, rb, t)
-            e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", INIT(rb) if ks == 0 else d)
+            e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", self.chain0(rb) if ks == 0 else d)
 
         if qk:
             for m in range(LEADK):
@@ -585,9 +622,12 @@ class FwdGen:
                         for i in range(16):
                             gy.add(f"mx{t}{rb}", 8, 16 * t - 1, 31,
                                    lambda rb=rb, t=t, i=i: self.mask_elem(nxt, rb, t, i))
-                    for (txt, d, srcs) in self.max_ops(nxt, rb, t):
-                        gy.add(f"mx{t}{rb}", 4, 16 * t - 1, 31,
-                               lambda txt=txt, d=d, srcs=srcs: e.valu(txt, d, srcs))
+                    for op in self.max_ops_z(nxt, rb, t):
+                        if op[0] == "max":
+                            gy.add(f"mx{t}{rb}", 4, 16 * t - 1, 31,
+                                   lambda op=op: e.valu(op[1], op[2], op[3]))
+                        else:
+                            gy.add(f"mx{t}{rb}", 4, 16 * t - 1, 31, lambda op=op: self.fma_z(nxt, *op[1:]))
         for n, el in enumerate(E):
             gy.add(f"add{n % 2}", 4, 0, 31, lambda el=el, c=n % 2: self.add(cur, el, c))
 
@@ -747,15 +787,16 @@ class FwdGen:
 # dK / dV (the backward's dominant kernel): dkdv_hp_kernel (csrc/dkdv_hp_kernel.h)
 #
 # Register map of the statement:
-#   v[0:31]     S[kb] accumulators (start as LSE2 rows), then P = exp2(-acc) in place
+#   v[0:31]     S[kb] accumulators, then P = exp2(acc scale log2 e - LSE2) in place
 #   v[32:63]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place
 #   v[64:79]    PP[kb][sp] packed P (B operand of dV^T += dO^T P), v[80:95] DSP[kb][sp] packed dS
 #   v[96:111]   row-fragment ring (Q then dO, A operands of S and dP), 4 slots
-#   v[112:135]  V fragment ring (B operands of dP), 6 slots
-#   v[136:151]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
-#   v[152:155]  mask bounds LO[kb], HI[kb] of a masked step
+#   v[112:131]  V fragment ring (B operands of dP), 5 slots
+#   v[132:147]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
+#   v[148:151]  mask bounds LO[kb], HI[kb] of a masked step
+#   v[152:167]  LSE2 of the 16 rows of this lane's registers (read per step from LDS)
 #   a[0:127]    dV^T[kb][dt], a[128:255] dK^T[kb][dt]
-#   K' = -(softmax_scale log2 e) K fragments: compiler-placed "v" operands %[k0]..%[k15]
+#   K fragments: compiler-placed "v" operands %[k0]..%[k15]
 # LDS (bytes from the workgroup's base): Q tile of buffer b at 16384 b, dO tile at 16384 b + 8192
 # (Tile<128, 32>), V rows of wave w at 32768 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of
 # buffer b at 98304 + 256 b (+128).
@@ -781,7 +822,7 @@ def DRR(n):
     return rng("v", 96 + 4 * (n % 4), 4)
 
 
-DVF_SLOTS = 6
+DVF_SLOTS = 5
 
 
 def DVF(n):
@@ -789,13 +830,20 @@ def DVF(n):
 
 
 def DTR(n, half=None):
-    base = 136 + 4 * (n % 4)
+    base = 132 + 4 * (n % 4)
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-DLO = ["v152", "v153"]
-DHI = ["v154", "v155"]
-DK_NVGPR = 156
+DLO = ["v148", "v149"]
+DHI = ["v150", "v151"]
+
+
+def DLSE(i):
+    """LSE2 of the row of register i (rows (i & 3) + 8 (i >> 2) + 4 hh of the step's tile)."""
+    return f"v{152 + i}"
+
+
+DK_NVGPR = 168
 
 
 def DDV(kb, dt):
@@ -868,9 +916,10 @@ class DkdvGen:
         self.e.ds_read(f"ds_read_b64_tr_b16 {d}, {base} offset:{imm}", d)
 
     def init_read(self, par, what, kb, g4):
-        """LSE2 (what 0) rows into S[kb], -delta (what 1) into dP[kb]: register group g4."""
+        """LSE2 (what 0) rows into the LSE registers, -delta (what 1) into dP[kb] (the dP
+        chain's initial accumulator): register group g4."""
         imm = par * 256 + what * 128 + 32 * g4
-        d = rng("v", (0 if what == 0 else 32) + 16 * kb + 4 * g4, 4)
+        d = rng("v", 152 + 4 * g4, 4) if what == 0 else rng("v", 32 + 16 * kb + 4 * g4, 4)
         self.e.ds_read(f"ds_read_b128 {d}, %[lb] offset:{imm}", d)
 
     def descriptors(self):
@@ -978,12 +1027,12 @@ class DkdvGen:
                     e.valu(f"v_subrev_u32 {DLO[kb]}, {D_CM}, %[lo{kb}]", DLO[kb], [])
                     e.valu(f"v_subrev_u32 {DHI[kb]}, {D_CM}, %[hi{kb}]", DHI[kb], [])
             g = GapScheduler(64)
-            # LSE2 rows into S[kb] (before the first S MFMA), -delta rows into dP[kb]
-            for what in range(2):
-                for kb in range(2):
-                    for g4 in range(4):
-                        rel, dl = (-1, -1) if what == 0 else (-1, 12)
-                        g.add(f"init{what}", 4, rel, dl, lambda what=what, kb=kb, g4=g4: self.init_read(par, what, kb, g4))
+            # LSE2 rows (used by the exponentials), -delta rows into dP[kb] (before the dP chains)
+            for g4 in range(4):
+                g.add("init0", 4, -1, 10, lambda g4=g4: self.init_read(par, 0, 0, g4))
+            for kb in range(2):
+                for g4 in range(4):
+                    g.add("init1", 4, -1, 12, lambda kb=kb, g4=g4: self.init_read(par, 1, kb, g4))
             # row fragments: Q (S phase) then dO (dP phase), 3 ahead; V fragments 3 ahead
             for n in range(16):
                 mf = 2 * n  # first MFMA using it (S: 2 ks, dP: 16 + 2 ks)
@@ -998,8 +1047,11 @@ class DkdvGen:
                 for kb in range(2):
                     for i in range(8 * sp, 8 * sp + 8):
                         r = DS(kb, i)
+                        # P = exp2(s scale log2 e - LSE2), the scale applied in fp32
+                        g.add(f"exp{kb}", 4, 19, 26 + 8 * sp,
+                              lambda r=r, i=i: e.valu(f"v_fma_f32 {r}, {r}, %[sc], -{DLSE(i)}", r, [r, DLSE(i)]))
                         g.add(f"exp{kb}", 8, 19, 27 + 8 * sp,
-                              lambda r=r: e.valu(f"v_exp_f32_e64 {r}, -{r}", r, [r], kind="trans"))
+                              lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
                         if masked:
                             g.add(f"exp{kb}", 16, 19, 28 + 8 * sp, lambda kb=kb, i=i: self.mask_elem(kb, i))
                     for j in range(4):
@@ -1024,9 +1076,9 @@ class DkdvGen:
                 g.add("dma", c, 2, 40 + n, f)
 
             def mfma(i):
-                if i < 16:  # S[kb] += Q(ks) K'[kb](ks)
+                if i < 16:  # S[kb] += Q(ks) K[kb](ks)
                     ks, kb = i >> 1, i & 1
-                    e.mfma(self.mop, DS(kb), DRR(ks), f"%[k{kb * 8 + ks}]", DS(kb))
+                    e.mfma(self.mop, DS(kb), DRR(ks), f"%[k{kb * 8 + ks}]", "0" if ks == 0 else DS(kb))
                 elif i < 32:  # dP[kb] += dO(ks) V[kb](ks)
                     ks, kb = (i - 16) >> 1, i & 1
                     e.mfma(self.mop, DDP(kb), DRR(8 + ks), DVF(2 * ks + kb), DDP(kb))
@@ -1127,7 +1179,8 @@ def gen_dkdv_function(bf16, causal):
            [f'"s{i}"' for i in D_SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
     sops = ["ng", "nmt", "total", "c0", "c01", "c012", "mlast", "lq", "qrb", "orb", "qtile", "otile", "qwrap",
-            "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0"]
+            "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
+            "sc"]
     vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1", "ooff0", "ooff1", "lsoff",
             "lo0", "lo1", "hi0", "hi1"]
     src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
@@ -1167,7 +1220,7 @@ def gen_read_dkdv():
 #   v[128:159]  DSP[rb][kk] packed dS^T (B operand of dQ^T += K^T dS^T)
 #   v[160:175]  K row-fragment ring, v[176:191] V row-fragment ring, v[192:207] K^T ring
 #   v[208:209]  mask limits of a masked tile
-#   a[0:127]    dQ^T[rb][dt]; a[128:255] the Q' (= scale log2 e Q) and dO fragments ("a" operands)
+#   a[0:127]    dQ^T[rb][dt]; a[128:255] the Q and dO fragments ("a" operands)
 def QS(rb, h, i=None):
     base = (rb * 2 + h) * 16
     return rng("v", base, 16) if i is None else f"v{base + i}"
@@ -1305,7 +1358,7 @@ class DqGen:
                         r = QS(rb, h, i)
                         st = f"p{h}{rb}"
                         g.add(st, 4, rel0, 38 + 16 * h,
-                              lambda r=r, rb=rb: e.valu(f"v_sub_f32 {r}, {r}, %[lse{rb}]", r, [r]))
+                              lambda r=r, rb=rb: e.valu(f"v_fma_f32 {r}, {r}, %[sc], -%[lse{rb}]", r, [r]))
                         g.add(st, 8, rel0, 40 + 16 * h, lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
                         if masked:
                             g.add(st, 8, rel0, 41 + 16 * h, lambda rb=rb, h=h, i=i: self.mask_elem(rb, h, i))
@@ -1416,7 +1469,7 @@ def gen_dq_function(bf16, causal):
     qops = ", ".join(f'[q{i}] "a"(q[{i}])' for i in range(16))
     oops = ", ".join(f'[o{i}] "a"(o[{i}])' for i in range(16))
     vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1"]
-    sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi"]
+    sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi", "sc"]
     src = f"""// hand-placed dQ statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 FA2_DEV void {name}(const u32x4 (&q)[16], const u32x4 (&o)[16], const DqHpArgs& a) {{
   asm volatile(
@@ -1436,14 +1489,14 @@ def _asm_body(lines):
     return "\n".join(f'      "{l}\\n"' for l in lines)
 
 
-def gen_fwd_function(bf16, causal):
-    g = FwdGen(bf16, causal)
+def gen_fwd_function(bf16, causal, exact=True):
+    g = FwdGen(bf16, causal, exact)
     lines = g.build()
-    name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
+    name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
     clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
            [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
     qops = ", ".join(f'[q{i}] "a"(q[{i}])' for i in range(16))
-    src = f"""// hand-placed main loop ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+    src = f"""// hand-placed main loop ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 FA2_DEV void {name}(const u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]) {{
   asm volatile(
 {_asm_body(lines)}
@@ -1454,7 +1507,7 @@ FA2_DEV void {name}(const u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2],
         [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]),
         [na] "s"(a.na), [last] "s"(a.last), [ntiles] "s"(a.ntiles), [mask0] "s"(a.mask0),
         [tileb] "s"(a.tileb), [kbytes] "s"(a.kbytes), [mlds] "s"(a.mlds),
-        [klo] "s"(a.klo), [khi] "s"(a.khi), [vlo] "s"(a.vlo), [vhi] "s"(a.vhi)
+        [klo] "s"(a.klo), [khi] "s"(a.khi), [vlo] "s"(a.vlo), [vhi] "s"(a.vhi), [uz] "s"(a.uz)
       : {", ".join(clob)});
 }}
 """
@@ -1479,7 +1532,8 @@ def write_headers():
     out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
     for bf16 in (True, False):
         for causal in (True, False):
-            out.append(gen_fwd_function(bf16, causal))
+            for exact in (True, False):
+                out.append(gen_fwd_function(bf16, causal, exact))
     out.append(gen_read_o())
     out.append("}  // namespace fa2\n")
     text = "\n".join(out)
