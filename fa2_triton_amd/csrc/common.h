@@ -107,6 +107,18 @@ inline bool bias16_rows(const void* bias, int dtype, const int64_t* stride) {
   return bias && (dtype == 16 || dtype == 17) && ((uintptr_t)bias & 15) == 0 && stride[0] % 8 == 0 &&
          stride[1] % 8 == 0 && stride[2] % 8 == 0;
 }
+// host side: compute units of the current device (persistent grids), cached per device id
+inline int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
 
 // ---------------------------------------------------------------------------------------------
 // Cross-half exchange: returns {x of lanes 0-31, x of lanes 32-63} in every lane.

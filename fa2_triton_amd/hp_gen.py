@@ -263,7 +263,9 @@ SM0 = "s82"       # saved m0
 SVOTE = "s[84:85]"
 SVOTE2 = "s[86:87]"
 SMASK = ["s[88:89]", "s[90:91]"]
+SPAR = "s66"      # buffer parity of the current period: (i + boff) & 1
 SGPR_CLOBBER = list(range(64, 92))
+N_NEXT = 12 + 16  # vector-memory ops of the next-unit requests (3 tiles x 4 pieces, 16 Q loads)
 
 LEADK = 3  # K fragments in flight ahead of their MFMAs
 LEADV = 3
@@ -469,9 +471,10 @@ class FwdGen:
             for rb in range(2):
                 e.valu(f"v_fma_f32 {MX[rb]}, {MX[rb]}, %[uz], {INIT(rb, 0)}", MX[rb], [MX[rb], INIT(rb, 0)])
 
-    def rescale(self, st, lbl_skip=None):
+    def rescale(self, st, first=False):
         """Defer-max rescale: for each row block, m_new = max(m_run, mx + m_ref), m_use = m_new or
-        0 when -inf; O, l *= exp2(m_run - m_use); z of set st -= m_use - m_ref; INIT = -m_use."""
+        0 when -inf; O, l *= exp2(m_run - m_use); z of set st -= m_use - m_ref; INIT = -m_use.
+        first: the unit's first tile (O and l are still zero: nothing to scale)."""
         e = self.e
         t_new, t_use, t_alpha, t_shift = TMP[0], TMP[1], TMP[2], TMP[3]
         # free during a rescale: the row-max chains and the mask limits (MX is still read)
@@ -481,13 +484,14 @@ class FwdGen:
             e.valu(f"v_max_f32 {t_new}, {MRUN[rb]}, {t_new}", t_new, [MRUN[rb], t_new])
             e.valu(f"v_cmp_eq_f32_e32 vcc, {VNINF}, {t_new}", None, [VNINF, t_new])
             e.valu(f"v_cndmask_b32_e64 {t_use}, {t_new}, 0, vcc", t_use, [t_new])
-            e.valu(f"v_sub_f32 {t_alpha}, {MRUN[rb]}, {t_use}", t_alpha, [MRUN[rb], t_use])
-            e.valu(f"v_exp_f32 {t_alpha}, {t_alpha}", t_alpha, [t_alpha], kind="trans")
             e.valu(f"v_sub_f32 {t_shift}, {t_use}, {MREF[rb]}", t_shift, [t_use, MREF[rb]])
-            for c in range(2):
-                e.valu(f"v_mul_f32 {LSUM[rb][c]}, {t_alpha}, {LSUM[rb][c]}", LSUM[rb][c], [t_alpha, LSUM[rb][c]])
+            if not first:
+                e.valu(f"v_sub_f32 {t_alpha}, {MRUN[rb]}, {t_use}", t_alpha, [MRUN[rb], t_use])
+                e.valu(f"v_exp_f32 {t_alpha}, {t_alpha}", t_alpha, [t_alpha], kind="trans")
+                for c in range(2):
+                    e.valu(f"v_mul_f32 {LSUM[rb][c]}, {t_alpha}, {LSUM[rb][c]}", LSUM[rb][c], [t_alpha, LSUM[rb][c]])
             # O[rb] *= alpha, in groups of len(scratch)
-            regs = [O(rb, dt, i) for dt in range(4) for i in range(16)]
+            regs = [] if first else [O(rb, dt, i) for dt in range(4) for i in range(16)]
             g = len(scratch)
             for k in range(0, len(regs), g):
                 grp = regs[k:k + g]
@@ -529,13 +533,14 @@ class FwdGen:
 
     # -- phases --------------------------------------------------------------------------------
     def qk_prologue(self, st):
-        """S(0) = K(0) Q^T (+ INIT) into set st, fragments read LEADK ahead; no fillers."""
+        """S(0) = K(0) Q^T (+ INIT) into set st (K(0) in K buffer st), fragments read LEADK ahead;
+        no fillers."""
         e = self.e
         for m in range(LEADK):
-            self.k_read(0, m)
+            self.k_read(st, m)
         for m in range(16):
             if m + LEADK < 16:
-                self.k_read(0, m + LEADK)
+                self.k_read(st, m + LEADK)
             t, ks = m // 8, m % 8
             for rb in range(2):
                 d = S(st, rb, t)
@@ -559,7 +564,77 @@ class FwdGen:
                         self.fma_z(st, *op[1:])
         self.row_max_finish()
 
-    def period_xy(self, par, cls, tag):
+    def period_end(self, final):
+        e = self.e
+        e.salu(f"s_add_i32 {SI}, {SI}, 1")
+        e.salu(f"s_add_i32 {SN1}, {SN1}, 64")
+        e.salu(f"s_xor_b32 {SPAR}, {SPAR}, 1")
+        if final:
+            # the next unit's loads stay in flight across the epilogue (its statement waits)
+            e.drain_lds()
+            e.raw(f"s_waitcnt vmcnt({N_NEXT})")
+            e.raw("s_barrier")
+            e.reset()
+        else:
+            self.barrier()
+
+    def next_unit_items(self, par):
+        """The final period's requests: the NEXT unit's K(0) -> K buffer 1-par, V(0) -> V buffer
+        1-par, K(1) -> K buffer par (all free in the final period), and its Q fragments straight
+        into the Q accumulation registers (%[q*], read-write operands); N_NEXT vector-memory ops.
+        Without a next unit the descriptors have range 0 (no memory access)."""
+        e = self.e
+        pieces = [(1 - par, "k0"), (1 - par, "v0"), (par, "k1")]
+
+        def lds_of(buf, what, it):
+            return (32768 if what == "v0" else 0) + buf * 16384 + it * 4096
+
+        seq = [(buf, what, it) for buf, what in pieces for it in range(4)]
+        out = []
+
+        def desc(what):
+            # s[68:71] next K tile 0 / 1, s[72:75] next V tile 0
+            d = 72 if what == "v0" else 68
+            return f"s[{d}:{d + 3}]"
+
+        def build_desc():
+            e.salu("s_mov_b32 s68, %[nklo]")
+            e.salu("s_and_b32 s69, %[nkhi], 0xffff")
+            e.salu("s_mov_b32 s70, %[nkbytes]")
+            e.salu("s_mov_b32 s71, 0x20000")
+            e.salu("s_mov_b32 s72, %[nvlo]")
+            e.salu("s_and_b32 s73, %[nvhi], 0xffff")
+            e.salu("s_mov_b32 s74, %[nkbytes]")
+            e.salu("s_mov_b32 s75, 0x20000")
+        out.append((8, build_desc))
+        for n, (buf, what, it) in enumerate(seq):
+            def f(n=n, buf=buf, what=what, it=it):
+                if n == 0:
+                    e.salu(f"s_add_u32 m0, %[mlds], {lds_of(buf, what, it)}", m0=True)
+                if n == 8:  # tile 1 of K: one tile further, range one tile shorter
+                    e.salu("s_add_u32 s68, s68, %[tileb]")
+                    e.salu("s_addc_u32 s69, s69, 0")
+                    e.salu("s_sub_i32 s70, s70, %[tileb]")
+                    e.salu("s_max_i32 s70, s70, 0")
+                e.dma(f"buffer_load_dwordx4 %[off{it}], {desc(what)}, 0 offen lds")
+                if n + 1 < len(seq):
+                    e.salu(f"s_add_u32 m0, %[mlds], {lds_of(*seq[n + 1])}", m0=True)
+            out.append((16, f))
+
+        def qdesc():
+            e.salu("s_mov_b32 s72, %[nqlo]")
+            e.salu("s_and_b32 s73, %[nqhi], 0xffff")
+            e.salu("s_mov_b32 s74, %[nqbytes]")
+            e.salu("s_mov_b32 s75, 0x20000")
+        out.append((8, qdesc))
+        for rb in range(2):
+            for ks in range(8):
+                def f(rb=rb, ks=ks):
+                    e.raw(f"buffer_load_dwordx4 %[q{rb * 8 + ks}], %[nqo{rb}], s[72:75], 0 offen offset:{32 * ks}")
+                out.append((16, f))
+        return out
+
+    def period_xy(self, par, cls, tag, final=False):
         """One period i (parity par) of class A (tile i+1 live, unmasked), B (live, masked) or C
         (no tile i+1): phase X = QK^T(i+1) MFMAs with the exponentials of tile i, phase Y = PV(i)
         MFMAs with the row sums of tile i and the mask / row max of tile i+1.  The fillers of each
@@ -570,11 +645,14 @@ class FwdGen:
         qk = cls in ("A", "B")
         masked = cls == "B"
         E = elem_order()
-        self.descriptors()
+        if final:
+            dma = self.next_unit_items(par)
+        else:
+            self.descriptors()
+            dma = self.dma_stream(par)
         if masked:
             for rb in range(2):
                 e.valu(f"v_subrev_u32 {REL[rb]}, {SN1}, %[rel{rb}]", REL[rb], [])
-        dma = self.dma_stream(par)
         # ---------------- phase X ----------------
         n_x_exp = 56 if qk else 64
         gx = GapScheduler(32 if qk else 0)
@@ -585,7 +663,7 @@ class FwdGen:
         for n, el in enumerate(E[:n_x_exp]):
             gx.add("exp", 8, -1, (n * 30) // n_x_exp, lambda el=el: self.exp(cur, el))
         for n, f in enumerate(dma):
-            gx.add("dma", f[0], -1, 4 * n + 3, f[1])
+            gx.add("dma", f[0], -1, min(31, 4 * n + 3), f[1])
         cv = [(rb, kk, j) for kk in range(4 if not qk else 1) for rb in range(2) for j in range(4)]
         for n, c in enumerate(cv):
             gx.add("cvt", 4, -1, 31, lambda c=c: self.cvt(cur, *c))
@@ -640,9 +718,7 @@ class FwdGen:
         if qk:
             self.row_max_finish()
             self.vote_and_rescale(nxt, tag)
-        e.salu(f"s_add_i32 {SI}, {SI}, 1")
-        e.salu(f"s_add_i32 {SN1}, {SN1}, 64")
-        self.barrier()
+        self.period_end(final)
 
     def dma_stream(self, par):
         """The period's 8 LDS-DMA pieces as (cost, emit) items; each item issues its piece and
@@ -663,15 +739,17 @@ class FwdGen:
             out.append((16, f))
         return out
 
-    def period_d(self, par):
-        self.descriptors()
-        for _, f in self.dma_stream(par):
+    def period_d(self, par, final=False):
+        if final:
+            items = self.next_unit_items(par)
+        else:
+            self.descriptors()
+            items = self.dma_stream(par)
+        for _, f in items:
             f()
-        self.e.salu(f"s_add_i32 {SI}, {SI}, 1")
-        self.e.salu(f"s_add_i32 {SN1}, {SN1}, 64")
-        self.barrier()
+        self.period_end(final)
 
-    # -- the whole work item -------------------------------------------------------------------
+    # -- one work unit (256 query rows), persistent across units --------------------------------
     def build(self):
         e = self.e
         e.raw("s_nop 7")
@@ -684,7 +762,7 @@ class FwdGen:
             e.valu(f"v_mov_b32 {MREF[rb]}, 0", MREF[rb])
             for c in range(2):
                 e.valu(f"v_mov_b32 {LSUM[rb][c]}, 0", LSUM[rb][c])
-            for j in range(16):
+            for j in range(1 if self.exact else 16):
                 e.valu(f"v_mov_b32 {INIT(rb, j)}, 0", INIT(rb, j))
         for rb in range(2):
             for dt in range(4):
@@ -706,73 +784,96 @@ class FwdGen:
         e.salu(f"s_sub_i32 {SVR}, {SVR}, %[tileb]")
         e.salu(f"s_mov_b32 {SI}, 0")
         e.salu(f"s_mov_b32 {SN1}, 0")
-        # K(0), V(0), K(1) (requested before the statement) have landed
+        e.salu(f"s_mov_b32 {SPAR}, %[boff]")
+        # this unit's K(0), V(0), K(1) and Q (requested during the previous unit's final period,
+        # or before the statement) have landed
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
         e.reset()
-        # ---- prologue: S(0) ----
+        # ---- prologue: S(0) in set boff (K(0) in K buffer boff) ----
         e.raw("s_cmp_lt_i32 %[last], 0")
         e.raw("s_cbranch_scc1 .Lhp%=_pro_end")
-        self.qk_prologue(0)
-        e.drain_lds()
-        e.drain_mfma()  # both paths below start with every S(0) result readable
-        e.raw("s_cmp_eq_u32 %[mask0], 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_pro_plain")
-        self.max_mask_plain(0, True)
-        self.rescale(0)
-        e.raw("s_branch .Lhp%=_pro_end")
-        e.label(".Lhp%=_pro_plain")
-        self.max_mask_plain(0, False)
-        self.rescale(0)
+        for par in (0, 1):
+            e.label(f".Lhp%=_pro{par}")
+            if par == 0:
+                e.raw(f"s_cmp_eq_u32 {SPAR}, 1")
+                e.raw("s_cbranch_scc1 .Lhp%=_pro1")
+            self.qk_prologue(par)
+            e.drain_lds()
+            e.drain_mfma()  # both paths below start with every S(0) result readable
+            e.raw("s_cmp_eq_u32 %[mask0], 0")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_pro{par}_plain")
+            self.max_mask_plain(par, True)
+            self.rescale(par, first=True)
+            e.raw("s_branch .Lhp%=_pro_end")
+            e.label(f".Lhp%=_pro{par}_plain")
+            self.max_mask_plain(par, False)
+            self.rescale(par, first=True)
+            e.raw("s_branch .Lhp%=_pro_end")
         e.label(".Lhp%=_pro_end")
         e.drain_mfma()
         e.raw("s_barrier")  # every wave is done with K(0) before K(2) lands in its buffer
         e.reset()
         e.salu(f"s_mov_b32 {SN1}, 64")
-        # ---- class A: periods 0 .. na-1 (tile i+1 live and unmasked), unrolled by two ----
+        e.salu("s_add_i32 s67, %[ntiles], -1")  # s67: index of the final period
+        e.raw("s_cmp_lt_i32 s67, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_noper")
+        # ---- periods 0 .. ntiles-2: class by tile i+1, body by parity ----
         e.raw(".balignl 64, 0xbf800000", 0)  # loop head on a 64-byte boundary, padded with s_nop 0
-        e.label(".Lhp%=_A")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
-        e.raw("s_cbranch_scc1 .Lhp%=_B")
-        self.period_xy(0, "A", "a0")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
-        e.raw("s_cbranch_scc1 .Lhp%=_B")
-        self.period_xy(1, "A", "a1")
-        e.raw("s_branch .Lhp%=_A")
-        # ---- class B: periods na .. last-1 (tile i+1 masked) ----
-        e.label(".Lhp%=_B")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[last]")
-        e.raw("s_cbranch_scc1 .Lhp%=_C")
-        e.raw(f"s_bitcmp1_b32 {SI}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_B1")
-        self.period_xy(0, "B", "b0")
-        e.raw("s_branch .Lhp%=_B")
-        e.label(".Lhp%=_B1")
-        self.period_xy(1, "B", "b1")
-        e.raw("s_branch .Lhp%=_B")
-        # ---- class C: period last (softmax + PV of the last live tile) ----
-        e.label(".Lhp%=_C")
-        e.raw(f"s_cmp_lg_u32 {SI}, %[last]")
-        e.raw("s_cbranch_scc1 .Lhp%=_D")
-        e.raw(f"s_bitcmp1_b32 {SI}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_C1")
-        self.period_xy(0, "C", "c0")
-        e.raw("s_branch .Lhp%=_D")
-        e.label(".Lhp%=_C1")
-        self.period_xy(1, "C", "c1")
-        # ---- class D: DMA-only periods until the workgroup's last tile ----
-        e.label(".Lhp%=_D")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[ntiles]")
-        e.raw("s_cbranch_scc1 .Lhp%=_end")
-        e.raw(f"s_bitcmp1_b32 {SI}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_D1")
-        self.period_d(0)
-        e.raw("s_branch .Lhp%=_D")
-        e.label(".Lhp%=_D1")
-        self.period_d(1)
-        e.raw("s_branch .Lhp%=_D")
+        e.label(".Lhp%=_loop")
+        e.raw(f"s_cmp_ge_i32 {SI}, s67")
+        e.raw("s_cbranch_scc1 .Lhp%=_fin")
+        e.raw(f"s_cmp_lt_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsA")
+        e.raw(f"s_cmp_lt_i32 {SI}, %[last]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
+        e.raw(f"s_cmp_eq_u32 {SI}, %[last]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsC")
+        e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_D0")
+        e.raw("s_branch .Lhp%=_D1")
+        for cls in ("A", "B", "C"):
+            e.label(f".Lhp%=_cls{cls}")
+            e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+            e.raw(f"s_cbranch_scc0 .Lhp%=_{cls}1")
+            for par in (0, 1):
+                e.label(f".Lhp%=_{cls}{par}")
+                self.period_xy(par, cls, f"{cls.lower()}{par}")
+                e.raw("s_branch .Lhp%=_loop")
+        for par in (0, 1):
+            e.label(f".Lhp%=_D{par}")
+            self.period_d(par)
+            e.raw("s_branch .Lhp%=_loop")
+        # ---- the final period (i = ntiles - 1): class C or D, the next unit's requests ----
+        e.label(".Lhp%=_fin")
+        e.raw(f"s_cmp_eq_u32 {SI}, %[last]")
+        e.raw("s_cbranch_scc0 .Lhp%=_finD")
+        e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_finC1")
+        for par in (0, 1):
+            e.label(f".Lhp%=_finC{par}")
+            self.period_xy(par, "C", f"fc{par}", final=True)
+            e.raw("s_branch .Lhp%=_end")
+        e.label(".Lhp%=_finD")
+        e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_finD1")
+        for par in (0, 1):
+            e.label(f".Lhp%=_finD{par}")
+            self.period_d(par, final=True)
+            e.raw("s_branch .Lhp%=_end")
+        # ---- no period at all: the next unit's requests right away (every buffer is free) ----
+        e.label(".Lhp%=_noper")
+        e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_noper1")
+        for par in (0, 1):
+            # parity of a virtual final period: boff ^ 1
+            if par == 1:
+                e.label(".Lhp%=_noper1")
+            for _, f in self.next_unit_items(par):
+                f()
+            e.raw("s_branch .Lhp%=_end")
         e.label(".Lhp%=_end")
-        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.drain_lds()
         for rb in range(2):
             e.valu(f"v_mov_b32 %[mo{rb}], {MRUN[rb]}", None, [MRUN[rb]])
             e.valu(f"v_add_f32 %[lo{rb}], {LSUM[rb][0]}, {LSUM[rb][1]}", None, LSUM[rb])
@@ -780,7 +881,6 @@ class FwdGen:
         e.raw("s_nop 15")
         e.raw("s_nop 15")
         return e.out
-
 
 
 # ----------------------------------------------------------------------------------------------
@@ -1495,19 +1595,22 @@ def gen_fwd_function(bf16, causal, exact=True):
     name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
     clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
            [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
-    qops = ", ".join(f'[q{i}] "a"(q[{i}])' for i in range(16))
-    src = f"""// hand-placed main loop ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
-FA2_DEV void {name}(const u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]) {{
+    qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
+    src = f"""// hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+// q: this unit's Q fragments in, the NEXT unit's Q fragments out -- still in flight (the next
+// statement waits for them first; nothing may read q in between)
+FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]) {{
   asm volatile(
 {_asm_body(lines)}
-      : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1])
-      : {qops},
-        [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),
+      : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1]), {qops}
+      : [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),
         [off0] "v"(a.off[0]), [off1] "v"(a.off[1]), [off2] "v"(a.off[2]), [off3] "v"(a.off[3]),
-        [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]),
+        [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]), [nqo0] "v"(a.nqo[0]), [nqo1] "v"(a.nqo[1]),
         [na] "s"(a.na), [last] "s"(a.last), [ntiles] "s"(a.ntiles), [mask0] "s"(a.mask0),
         [tileb] "s"(a.tileb), [kbytes] "s"(a.kbytes), [mlds] "s"(a.mlds),
-        [klo] "s"(a.klo), [khi] "s"(a.khi), [vlo] "s"(a.vlo), [vhi] "s"(a.vhi), [uz] "s"(a.uz)
+        [klo] "s"(a.klo), [khi] "s"(a.khi), [vlo] "s"(a.vlo), [vhi] "s"(a.vhi), [uz] "s"(a.uz),
+        [boff] "s"(a.boff), [nklo] "s"(a.nklo), [nkhi] "s"(a.nkhi), [nvlo] "s"(a.nvlo), [nvhi] "s"(a.nvhi),
+        [nkbytes] "s"(a.nkbytes), [nqlo] "s"(a.nqlo), [nqhi] "s"(a.nqhi), [nqbytes] "s"(a.nqbytes)
       : {", ".join(clob)});
 }}
 """
