@@ -832,7 +832,20 @@ class FwdGen:
         e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
         e.raw("s_cbranch_scc1 .Lhp%=_D0")
         e.raw("s_branch .Lhp%=_D1")
-        for cls in ("A", "B", "C"):
+        # class A runs as a chain: one compare and one (mostly not taken) branch per period
+        e.label(".Lhp%=_clsA")
+        e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_A1")
+        e.label(".Lhp%=_A0")
+        self.period_xy(0, "A", "a0")
+        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_loop")
+        e.label(".Lhp%=_A1")
+        self.period_xy(1, "A", "a1")
+        e.raw(f"s_cmp_lt_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_A0")
+        e.raw("s_branch .Lhp%=_loop")
+        for cls in ("B", "C"):
             e.label(f".Lhp%=_cls{cls}")
             e.raw(f"s_cmp_eq_u32 {SPAR}, 0")
             e.raw(f"s_cbranch_scc0 .Lhp%=_{cls}1")
@@ -1359,6 +1372,9 @@ def QDQ(rb, dt):
 
 # scalar state of the dQ statement (shares the forward's cursor registers)
 Q_SN0 = "s66"  # first key of the current tile
+Q_PAR = "s67"  # buffer parity of the current tile: (i + boff) & 1
+Q_FIN = "s83"  # index of the unit's final tile
+Q_NA = "s84"   # class A tiles the A chain runs: min(na, final)
 
 
 class DqGen:
@@ -1495,11 +1511,28 @@ class DqGen:
             g.run(mfma, pre_budget=48)
         e.salu(f"s_add_i32 {SI}, {SI}, 1")
         e.salu(f"s_add_i32 {Q_SN0}, {Q_SN0}, 64")
+        e.salu(f"s_xor_b32 {Q_PAR}, {Q_PAR}, 1")
         e.drain_lds()
         e.raw("s_waitcnt vmcnt(0)")
         e.raw("s_barrier")
         e.reset()
 
+    def next_unit_loads(self):
+        """The next unit's Q and dO fragments straight into the %[q*] / %[o*] accumulation
+        registers (read-write operands; the caller waits before reading them).  Descriptor range
+        0 without a next unit."""
+        e = self.e
+        for what, d in (("q", 68), ("o", 72)):
+            e.salu(f"s_mov_b32 s{d}, %[n{what}lo]")
+            e.salu(f"s_and_b32 s{d + 1}, %[n{what}hi], 0xffff")
+            e.salu(f"s_mov_b32 s{d + 2}, %[n{what}bytes]")
+            e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+        for what, d in (("q", 68), ("o", 72)):
+            for rb in range(2):
+                for ks in range(8):
+                    e.raw(f"buffer_load_dwordx4 %[{what}{rb * 8 + ks}], %[n{what}o{rb}], s[{d}:{d + 3}], 0 offen offset:{32 * ks}")
+
+    # -- one unit (256 query rows), persistent across units -------------------------------------
     def build(self):
         e = self.e
         e.raw("s_nop 7")
@@ -1507,7 +1540,8 @@ class DqGen:
         e.salu(f"s_mov_b32 {SM0}, m0")
         for r in range(128):
             e.valu(f"v_accvgpr_write_b32 a{r}, 0", f"a{r}", kind="accw")
-        # DMA cursors: period i requests K(i + 1), V(i + 1)
+        # DMA cursors: period i requests K(i + 1), V(i + 1); the final period's requests are the
+        # next unit's K(0), V(0) (cursors switched to its slices), into the buffer it starts on
         e.salu(f"s_mov_b32 {SKP[0]}, %[klo]")
         e.salu(f"s_mov_b32 {SKP[1]}, %[khi]")
         e.salu(f"s_mov_b32 {SVP[0]}, %[vlo]")
@@ -1520,44 +1554,82 @@ class DqGen:
             e.salu(f"s_sub_i32 {rem}, {rem}, %[tileb]")
         e.salu(f"s_mov_b32 {SI}, 0")
         e.salu(f"s_mov_b32 {Q_SN0}, 0")
+        e.salu(f"s_mov_b32 {Q_PAR}, %[boff]")
+        e.salu(f"s_add_i32 {Q_FIN}, %[ntiles], -1")
+        e.salu(f"s_min_i32 {Q_NA}, %[na], {Q_FIN}")  # A chain: class A tiles before the final one
+        # this unit's K(0), V(0) (requested by the previous unit or before the statement), Q, dO
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
         e.reset()
+        e.raw(f"s_cmp_lt_i32 {Q_FIN}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_loop")
+        # no tile: the next unit's K(0), V(0) into buffer boff as a DMA-only period of parity 1-boff
+        self.switch_cursors()
+        e.salu(f"s_xor_b32 {Q_PAR}, {Q_PAR}, 1")
+        e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_D0")
+        e.raw("s_branch .Lhp%=_D1")
         e.raw(".balignl 64, 0xbf800000", 0)
-        e.label(".Lhp%=_A")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
-        e.raw("s_cbranch_scc1 .Lhp%=_B")
-        self.period(0, "A")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[na]")
-        e.raw("s_cbranch_scc1 .Lhp%=_B")
-        self.period(1, "A")
-        e.raw("s_branch .Lhp%=_A")
-        e.label(".Lhp%=_B")
-        e.raw(f"s_cmp_gt_i32 {SI}, %[last]")
-        e.raw("s_cbranch_scc1 .Lhp%=_D")
-        e.raw(f"s_bitcmp1_b32 {SI}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_B1")
-        self.period(0, "B")
-        e.raw("s_branch .Lhp%=_B")
-        e.label(".Lhp%=_B1")
-        self.period(1, "B")
-        e.raw("s_branch .Lhp%=_B")
-        e.label(".Lhp%=_D")
-        e.raw(f"s_cmp_ge_i32 {SI}, %[ntiles]")
+        e.label(".Lhp%=_loop")
+        e.raw(f"s_cmp_gt_i32 {SI}, {Q_FIN}")
         e.raw("s_cbranch_scc1 .Lhp%=_end")
-        e.raw(f"s_bitcmp1_b32 {SI}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_D1")
-        self.period(0, "D")
-        e.raw("s_branch .Lhp%=_D")
-        e.label(".Lhp%=_D1")
-        self.period(1, "D")
-        e.raw("s_branch .Lhp%=_D")
+        e.raw(f"s_cmp_eq_u32 {SI}, {Q_FIN}")
+        e.raw("s_cbranch_scc0 .Lhp%=_cls")
+        self.switch_cursors()
+        e.label(".Lhp%=_cls")
+        e.raw(f"s_cmp_lt_i32 {SI}, %[na]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsA")
+        e.raw(f"s_cmp_le_i32 {SI}, %[last]")
+        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
+        e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_D0")
+        e.raw("s_branch .Lhp%=_D1")
+        # class A runs as a chain (the final tile excluded: its cursors switch first)
+        e.label(".Lhp%=_clsA")
+        e.raw(f"s_cmp_eq_u32 {SI}, {Q_FIN}")
+        e.raw("s_cbranch_scc1 .Lhp%=_A1f")
+        e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_A1")
+        e.label(".Lhp%=_A0")
+        self.period(0, "A")
+        e.raw(f"s_cmp_ge_i32 {SI}, {Q_NA}")
+        e.raw("s_cbranch_scc1 .Lhp%=_loop")
+        e.label(".Lhp%=_A1")
+        self.period(1, "A")
+        e.raw(f"s_cmp_lt_i32 {SI}, {Q_NA}")
+        e.raw("s_cbranch_scc1 .Lhp%=_A0")
+        e.raw("s_branch .Lhp%=_loop")
+        e.label(".Lhp%=_A1f")  # the final tile, class A: parity dispatch
+        e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+        e.raw("s_cbranch_scc1 .Lhp%=_A0")
+        e.raw("s_branch .Lhp%=_A1")
+        e.label(".Lhp%=_clsB")
+        e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+        e.raw("s_cbranch_scc0 .Lhp%=_B1")
+        for par in (0, 1):
+            e.label(f".Lhp%=_B{par}")
+            self.period(par, "B")
+            e.raw("s_branch .Lhp%=_loop")
+        for par in (0, 1):
+            e.label(f".Lhp%=_D{par}")
+            self.period(par, "D")
+            e.raw("s_branch .Lhp%=_loop")
         e.label(".Lhp%=_end")
-        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.next_unit_loads()
+        e.drain_lds()
         e.salu(f"s_mov_b32 m0, {SM0}")
         e.raw("s_nop 15")
         e.raw("s_nop 15")
         return e.out
+
+    def switch_cursors(self):
+        e = self.e
+        e.salu(f"s_mov_b32 {SKP[0]}, %[nklo]")
+        e.salu(f"s_mov_b32 {SKP[1]}, %[nkhi]")
+        e.salu(f"s_mov_b32 {SVP[0]}, %[nvlo]")
+        e.salu(f"s_mov_b32 {SVP[1]}, %[nvhi]")
+        e.salu(f"s_mov_b32 {SKR}, %[nkbytes]")
+        e.salu(f"s_mov_b32 {SVR}, %[nkbytes]")
 
 
 def gen_dq_function(bf16, causal):
@@ -1566,18 +1638,21 @@ def gen_dq_function(bf16, causal):
     name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     clob = [f'"v{i}"' for i in range(DQ_NVGPR)] + [f'"a{i}"' for i in range(128)] + \
            [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
-    qops = ", ".join(f'[q{i}] "a"(q[{i}])' for i in range(16))
-    oops = ", ".join(f'[o{i}] "a"(o[{i}])' for i in range(16))
-    vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1"]
-    sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi", "sc"]
-    src = f"""// hand-placed dQ statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
-FA2_DEV void {name}(const u32x4 (&q)[16], const u32x4 (&o)[16], const DqHpArgs& a) {{
+    qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
+    oops = ", ".join(f'[o{i}] "+a"(o[{i}])' for i in range(16))
+    vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1",
+            "nqo0", "nqo1", "noo0", "noo1"]
+    sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi", "sc",
+            "boff", "nklo", "nkhi", "nvlo", "nvhi", "nkbytes", "nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes"]
+    src = f"""// hand-placed dQ unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+// q / o: this unit's Q and dO fragments in, the NEXT unit's out -- still in flight (wait before
+// reading them)
+FA2_DEV void {name}(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a) {{
   asm volatile(
 {_asm_body(lines)}
-      :
       : {qops},
-        {oops},
-        {", ".join(f'[{n}] "v"(a.{n})' for n in vops)},
+        {oops}
+      : {", ".join(f'[{n}] "v"(a.{n})' for n in vops)},
         {", ".join(f'[{n}] "s"(a.{n})' for n in sops)}
       : {", ".join(clob)});
 }}
