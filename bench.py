@@ -485,8 +485,10 @@ def main():
     # device symbols the workload dispatches to (the pipelined forward: aligned D, no bias, no dropout)
     hp_fwd = plain and d == 128 and os.environ.get("FA2_FWD_HP", "1") != "0"
     hp_dkdv = plain and d == 128 and os.environ.get("FA2_DKDV_HP", "1") != "0"
+    hp_dq = plain and d == 128 and os.environ.get("FA2_DQ_HP", "1") != "0"
     symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if plain else "fwd_kernel"),
-              "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel", "dq_kernel": "dq_kernel"}
+              "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel",
+              "dq_kernel": "dq_hp_kernel" if hp_dq else "dq_kernel"}
     esz = q.element_size()
 
     def roofline(name):

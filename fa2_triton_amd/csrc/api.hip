@@ -7,6 +7,9 @@
 #include <stdio.h>
 
 #include "fa2_internal.h"
+#if FA2_HP_STAMPS
+#include "common.h"
+#endif
 
 namespace {
 
@@ -168,5 +171,17 @@ int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32
   return hip_status(fa2::launch_cu_seqlens(mask, mask_row_stride, batch, seqlen, cu_seqlens, (hipStream_t)stream),
                     "fa2_cu_seqlens_from_mask launch");
 }
+
+#if FA2_HP_STAMPS
+// development builds only (not part of the C ABI in include/fa2_amd.h): read and clear the
+// hand-placed kernels' s_memtime sums
+int fa2_debug_hp_stamps(unsigned long long* out16) {
+  unsigned long long* b = fa2::hp_stamp_buf();
+  if (!b || !out16) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out16, b, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(b, 0, 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // extern "C"

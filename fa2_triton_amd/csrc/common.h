@@ -107,6 +107,16 @@ inline bool bias16_rows(const void* bias, int dtype, const int64_t* stride) {
   return bias && (dtype == 16 || dtype == 17) && ((uintptr_t)bias & 15) == 0 && stride[0] % 8 == 0 &&
          stride[1] % 8 == 0 && stride[2] % 8 == 0;
 }
+#if FA2_HP_STAMPS
+// development builds (-DFA2_HP_STAMPS=1): per-wave s_memtime sums of the hand-placed kernels,
+// accumulated into one device buffer of 16 counters (fa2_debug_hp_stamps reads and clears it)
+inline unsigned long long* hp_stamp_buf() {
+  static unsigned long long* buf = nullptr;
+  if (!buf && hipMalloc((void**)&buf, 16 * sizeof(unsigned long long)) == hipSuccess)
+    (void)hipMemset(buf, 0, 16 * sizeof(unsigned long long));
+  return buf;
+}
+#endif
 // host side: compute units of the current device (persistent grids), cached per device id
 inline int device_cu_count() {
   static int cached[64] = {0};
@@ -519,11 +529,18 @@ FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool vali
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const int c = lane % CPR;
+  // every row read issued before the first store (one LDS wait, not one per store)
+  u32x4 v[32 / RPI];
 #pragma unroll
   for (int j = 0; j < 32 / RPI; ++j) {
     const int R = j * RPI + lane / CPR;
-    const u32x4 v = *(const u32x4*)(stage + R * (DT * 2) + 16 * (c ^ (R % CPR)));
-    if (R < nrows && 8 * c < D) *(u32x4*)(g0 + (int64_t)R * rstride + 8 * c) = v;
+    v[j] = *(const u32x4*)(stage + R * (DT * 2) + 16 * (c ^ (R % CPR)));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int j = 0; j < 32 / RPI; ++j) {
+    const int R = j * RPI + lane / CPR;
+    if (R < nrows && 8 * c < D) *(u32x4*)(g0 + (int64_t)R * rstride + 8 * c) = v[j];
   }
 }
 

@@ -352,8 +352,8 @@ class FwdGen:
     with -m_ref, so the chain yields z directly (no per-score VALU; costs one extra rounding of
     the scores, ~2^-9 relative in bf16)."""
 
-    def __init__(self, bf16, causal, exact=True):
-        self.bf16, self.causal, self.exact = bf16, causal, exact
+    def __init__(self, bf16, causal, exact=True, stamp=False):
+        self.bf16, self.causal, self.exact, self.stamp = bf16, causal, exact, stamp
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
@@ -526,9 +526,20 @@ class FwdGen:
 
     def barrier(self):
         e = self.e
+        if self.stamp:  # s98 += wait for own LDS reads + DMA, s99 += barrier (dev builds only)
+            e.raw("s_memtime s[92:93]")
         e.drain_lds()
         e.raw("s_waitcnt vmcnt(0)")
+        if self.stamp:
+            e.raw("s_memtime s[94:95]")
         e.raw("s_barrier")
+        if self.stamp:
+            e.raw("s_memtime s[96:97]")
+            e.raw("s_waitcnt lgkmcnt(0)")
+            e.raw("s_sub_u32 s92, s94, s92")
+            e.raw("s_add_u32 s98, s98, s92")
+            e.raw("s_sub_u32 s92, s96, s94")
+            e.raw("s_add_u32 s99, s99, s92")
         e.reset()
 
     # -- phases --------------------------------------------------------------------------------
@@ -754,6 +765,10 @@ class FwdGen:
         e = self.e
         e.raw("s_nop 7")
         e.raw("s_nop 7")
+        if self.stamp:
+            e.raw("s_memtime s[100:101]")
+            e.raw("s_mov_b32 s98, 0")
+            e.raw("s_mov_b32 s99, 0")
         e.salu(f"s_mov_b32 {SM0}, m0")
         e.valu(f"v_mov_b32 {VNINF}, {NINF}", VNINF)
         for rb in range(2):
@@ -789,6 +804,11 @@ class FwdGen:
         # or before the statement) have landed
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
+        if self.stamp:  # prologue wait
+            e.raw("s_memtime s[92:93]")
+            e.raw("s_waitcnt lgkmcnt(0)")
+            e.raw("s_sub_u32 s92, s92, s100")
+            e.raw("s_mov_b32 %[st2], s92")
         e.reset()
         # ---- prologue: S(0) in set boff (K(0) in K buffer boff) ----
         e.raw("s_cmp_lt_i32 %[last], 0")
@@ -891,6 +911,13 @@ class FwdGen:
             e.valu(f"v_mov_b32 %[mo{rb}], {MRUN[rb]}", None, [MRUN[rb]])
             e.valu(f"v_add_f32 %[lo{rb}], {LSUM[rb][0]}, {LSUM[rb][1]}", None, LSUM[rb])
         e.salu(f"s_mov_b32 m0, {SM0}")
+        if self.stamp:
+            e.raw("s_memtime s[92:93]")
+            e.raw("s_waitcnt lgkmcnt(0)")
+            e.raw("s_sub_u32 s92, s92, s100")
+            e.raw("s_mov_b32 %[st0], s98")
+            e.raw("s_mov_b32 %[st1], s99")
+            e.raw("s_mov_b32 %[st3], s92")
         e.raw("s_nop 15")
         e.raw("s_nop 15")
         return e.out
@@ -1311,16 +1338,20 @@ FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
 
 
 def gen_read_dkdv():
-    parts = ["// dV^T a[0:127], dK^T a[128:255] -> registers (after the statement's final drain)",
-             "FA2_DEV void dkdv_hp_read(f32x16 (&dv)[2][4], f32x16 (&dk)[2][4]) {"]
-    for which, base0 in (("dv", 0), ("dk", 128)):
-        for kb in range(2):
+    parts = ["// dV^T a[0:127], dK^T a[128:255] of key block KB -> registers (after the statement's final",
+             "// drain); one key block at a time keeps the epilogue within the register file",
+             "template <int KB>",
+             "FA2_DEV void dkdv_hp_read(f32x16 (&dv)[4], f32x16 (&dk)[4]);"]
+    for kb in range(2):
+        parts.append("template <>")
+        parts.append(f"FA2_DEV void dkdv_hp_read<{kb}>(f32x16 (&dv)[4], f32x16 (&dk)[4]) {{")
+        for which, base0 in (("dv", 0), ("dk", 128)):
             for dt in range(4):
                 base = base0 + (kb * 4 + dt) * 16
-                outs = ", ".join(f'"=v"({which}[{kb}][{dt}][{i}])' for i in range(16))
+                outs = ", ".join(f'"=v"({which}[{dt}][{i}])' for i in range(16))
                 body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
                 parts.append(f'  asm volatile("{body}" : {outs});')
-    parts.append("}")
+        parts.append("}")
     return "\n".join(parts) + "\n"
 
 
@@ -1665,19 +1696,25 @@ def _asm_body(lines):
 
 
 def gen_fwd_function(bf16, causal, exact=True):
-    g = FwdGen(bf16, causal, exact)
-    lines = g.build()
-    name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
-    clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
-           [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
-    qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
-    src = f"""// hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+    out = []
+    for stamp in (False, True):
+        g = FwdGen(bf16, causal, exact, stamp)
+        lines = g.build()
+        name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
+        sg = SGPR_CLOBBER + (list(range(92, 102)) if stamp else [])
+        clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
+               [f'"s{i}"' for i in sg] + ['"vcc"', '"scc"', '"memory"']
+        qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
+        stops = ", " + ", ".join(f'[st{i}] "=&s"(st[{i}])' for i in range(4)) if stamp else ""
+        starg = ", uint32_t (&st)[4]" if stamp else ""
+        out.append(f"""{'#if FA2_HP_STAMPS' if stamp else '#if !FA2_HP_STAMPS'}
+// hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}{', stamped' if stamp else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 // q: this unit's Q fragments in, the NEXT unit's Q fragments out -- still in flight (the next
 // statement waits for them first; nothing may read q in between)
-FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]) {{
+FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]{starg}) {{
   asm volatile(
 {_asm_body(lines)}
-      : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1]), {qops}
+      : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1]), {qops}{stops}
       : [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),
         [off0] "v"(a.off[0]), [off1] "v"(a.off[1]), [off2] "v"(a.off[2]), [off3] "v"(a.off[3]),
         [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]), [nqo0] "v"(a.nqo[0]), [nqo1] "v"(a.nqo[1]),
@@ -1688,8 +1725,9 @@ FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float
         [nkbytes] "s"(a.nkbytes), [nqlo] "s"(a.nqlo), [nqhi] "s"(a.nqhi), [nqbytes] "s"(a.nqbytes)
       : {", ".join(clob)});
 }}
-"""
-    return src
+#endif
+""")
+    return "".join(out)
 
 
 def gen_read_o():
