@@ -324,6 +324,8 @@ def main():
     ap.add_argument("--no-causal", dest="causal", action="store_false")
     ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--bias", action="store_true", help="[1, 1, Sq, Sk] additive bias in the input dtype")
+    ap.add_argument("--bias-grad", action="store_true",
+                    help="--bias that requires grad: the backward also computes dBias (library extension)")
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo: sharding + timing plumbing, no kernels")
@@ -394,7 +396,12 @@ def main():
     k = torch.empty(b, s, hkv, d, device=device, dtype=dtype).normal_(0, 0.5).requires_grad_(not fwd_only)
     v = torch.empty(b, s, hkv, d, device=device, dtype=dtype).normal_(0, 0.5).requires_grad_(not fwd_only)
     do = torch.randn(b, s, h, d, device=device, dtype=dtype)
+    if args.bias_grad:
+        args.bias = True
     bias = torch.rand(1, 1, s, s, device=device, dtype=dtype) if args.bias else None
+    if bias is not None and args.bias_grad and not fwd_only:
+        bias.requires_grad_(True)
+    grad_inputs = (q, k, v, bias) if bias is not None and bias.requires_grad else (q, k, v)
     p_drop = args.dropout
     seed = DROPOUT_SEED if p_drop > 0 else None
 
@@ -404,7 +411,7 @@ def main():
                 flash_attn_func(q, k, v, None, bias, p_drop, causal, None, seed)
         else:
             out = flash_attn_func(q, k, v, None, bias, p_drop, causal, None, seed)
-            torch.autograd.grad(out, (q, k, v), do)
+            torch.autograd.grad(out, grad_inputs, do)
 
     for _ in range(args.warmup):
         step()
@@ -439,12 +446,15 @@ def main():
 
         def bwd(stages):
             return lambda: _flash_attn_backward(do, q, k, v, bias, None, o, lse, p_drop, causal, None, seed,
-                                                _stages=stages, _delta=delta, dropout_mask=kmask)
+                                                _stages=stages, _delta=delta, dropout_mask=kmask,
+                                                bias_grad=stages == 8)
 
         calls = {"fwd_kernel": lambda: _flash_attn_forward(q, k, v, None, bias, p_drop, causal, None, seed,
                                                            dropout_mask=kmask)}
         if not fwd_only:
             calls.update(dq_kernel=bwd(4), dkdv_kernel=bwd(2))
+            if bias is not None and bias.requires_grad:
+                calls.update(dbias_kernel=bwd(8))
         times, spread = {}, {}
         for name, fn in calls.items():
             fn()
@@ -467,6 +477,8 @@ def main():
     # (0.5 F).  The dQ kernel also recomputes S and dP (1 F executed, not algorithmic).
     algo = {"fwd_kernel": f_fwd, "dkdv_kernel": 2.0 * f_fwd, "dq_kernel": 0.5 * f_fwd}
     executed = dict(algo, dq_kernel=1.5 * f_fwd)
+    if "dbias_kernel" in times:  # dBias (extension): S and dP recomputed, counted as its own work
+        algo["dbias_kernel"] = executed["dbias_kernel"] = f_fwd
     kernels = {
         name: {
             "ms": round(t * 1e3, 4),
@@ -488,7 +500,7 @@ def main():
     hp_dq = plain and d == 128 and os.environ.get("FA2_DQ_HP", "1") != "0"
     symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if plain else "fwd_kernel"),
               "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel",
-              "dq_kernel": "dq_hp_kernel" if hp_dq else "dq_kernel"}
+              "dq_kernel": "dq_hp_kernel" if hp_dq else "dq_kernel", "dbias_kernel": "dbias_kernel"}
     esz = q.element_size()
 
     def roofline(name):

@@ -1356,10 +1356,11 @@ static hipError_t launch_bwd_t(const fa2_bwd_args& a, int stages, hipStream_t st
     hipLaunchKernelGGL((delta_kernel<BF16, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if ((stages & 4) && a.seqlen_q > 0) {
-    if constexpr (DT == 128 && !BIAS && !DROPOUT && ALIGNED) {
-      // hand-placed one-wave-per-SIMD dQ (dq_hp_kernel.h) for D = 128 exactly
+    if constexpr (DT == 128 && !BIAS && ALIGNED) {
+      // hand-placed one-wave-per-SIMD dQ (dq_hp_kernel.h) for D = 128 exactly (dropout: with
+      // the forward's saved keep words)
       if (dq_hp_ok(a, true)) {
-        launch_dq_hp<BF16, CAUSAL>(a, st);
+        launch_dq_hp<BF16, CAUSAL, DROPOUT>(a, st);
         goto dq_done;
       }
     }

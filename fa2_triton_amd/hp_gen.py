@@ -1350,7 +1350,8 @@ def gen_read_dkdv():
                 base = base0 + (kb * 4 + dt) * 16
                 outs = ", ".join(f'"=v"({which}[{dt}][{i}])' for i in range(16))
                 body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
-                parts.append(f'  asm volatile("{body}" : {outs});')
+                clob = ", ".join(f'"a{r}"' for r in range(256))
+                parts.append(f'  asm volatile("{body}" : {outs} : : {clob});')
         parts.append("}")
     return "\n".join(parts) + "\n"
 
@@ -1395,6 +1396,22 @@ def QTR(n, half=None):
 
 QREL = ["v208", "v209"]
 DQ_NVGPR = 210
+# dropout (the forward's saved keep words, one 32-key word per row): the words of the current and
+# the next tile, per (rb, key half h); per-stream temporaries; the lane's word offsets (cursor)
+def QMW(st, rb, h):
+    return f"v{210 + 4 * st + 2 * rb + h}"
+
+
+def QMT(h, rb):
+    """dS temporaries: the K ring's slot 0, free once the S chains are issued (the dS phase
+    starts 18 MFMAs later)."""
+    return f"v{160 + 2 * h + rb}"
+
+
+QMO = "v218"       # lane byte offset of row block 0's tile-0 words (row block 1: + %[mrs])
+DQ_NVGPR_DROP = 219
+Q_MD = "s[92:95]"  # keep-word descriptor
+Q_MOFF = ["s96", "s97"]  # byte offsets of the requested tile's words, row block 0 / 1
 
 
 def QDQ(rb, dt):
@@ -1415,11 +1432,27 @@ class DqGen:
     Same math as the reference's dQ loop (/root/reference/src/backward/compute_dq.py:38-78)
     and dq_kernel: P = exp2(s scale log2 e - LSE2), dS = P (dP - delta), dQ = scale dS K."""
 
-    def __init__(self, bf16, causal):
-        self.bf16, self.causal = bf16, causal
+    def __init__(self, bf16, causal, dropout=False):
+        self.bf16, self.causal, self.dropout = bf16, causal, dropout
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
+
+    def mask_items(self, par):
+        """Dropout: the keep words of the next tile (rows of rb, keys 32 h ..) into set 1 - par;
+        four dword loads, then the cursor moves one tile (64 keys = 2 words = 256 bytes per row
+        block tile of 32 rows)."""
+        e = self.e
+        out = []
+        for rb in range(2):
+            for h in range(2):
+                def f(rb=rb, h=h):
+                    e.raw(f"buffer_load_dword {QMW(1 - par, rb, h)}, {QMO}, {Q_MD}, {Q_MOFF[rb]} offen offset:{128 * h}")
+                    if rb == 1 and h == 1:
+                        e.salu(f"s_add_u32 {Q_MOFF[0]}, {Q_MOFF[0]}, 256")
+                        e.salu(f"s_add_u32 {Q_MOFF[1]}, {Q_MOFF[1]}, 256")
+                out.append((16, f))
+        return out
 
     def k_read(self, par, n):
         h, ks = n // 8, n % 8
@@ -1476,7 +1509,7 @@ class DqGen:
     def period(self, par, cls):
         e = self.e
         self.descriptors()
-        dma = self.dma_items(par)
+        dma = self.dma_items(par) + (self.mask_items(par) if self.dropout else [])
         if cls == "D":
             for _, f in dma:
                 f()
@@ -1511,11 +1544,25 @@ class DqGen:
                             g.add(st, 8, rel0, 41 + 16 * h, lambda rb=rb, h=h, i=i: self.mask_elem(rb, h, i))
                 rel1 = 50 + 16 * h
                 for rb in range(2):
+                    if self.dropout:  # this lane's keys start 4 hh into the word
+                        w_ = QMW(par, rb, h)
+                        g.add(f"d{h}{rb}", 4, -1, rel1,
+                              lambda w_=w_: e.valu(f"v_lshrrev_b32 {w_}, %[msh], {w_}", w_, [w_]))
                     for i in range(16):
                         a_, b_ = QS(rb, h, i), QDP(rb, h, i)
                         st = f"d{h}{rb}"
-                        g.add(st, 4, rel1, 58 + 16 * h,
-                              lambda b_=b_, rb=rb: e.valu(f"v_sub_f32 {b_}, {b_}, %[del{rb}]", b_, [b_]))
+                        if self.dropout:
+                            # dS = P (dP M / (1 - p) - delta), M the forward's keep bit
+                            t_, w_, k_ = QMT(h, rb), QMW(par, rb, h), (i & 3) + 8 * (i >> 2)
+                            g.add(st, 4, rel1, 56 + 16 * h,
+                                  lambda t_=t_, w_=w_, k_=k_: e.valu(f"v_bfe_i32 {t_}, {w_}, {k_}, 1", t_, [w_]))
+                            g.add(st, 4, rel1, 57 + 16 * h,
+                                  lambda t_=t_, b_=b_: e.valu(f"v_and_b32 {b_}, {t_}, {b_}", b_, [t_, b_]))
+                            g.add(st, 4, rel1, 58 + 16 * h,
+                                  lambda b_=b_, rb=rb: e.valu(f"v_fma_f32 {b_}, {b_}, %[dsc], -%[del{rb}]", b_, [b_]))
+                        else:
+                            g.add(st, 4, rel1, 58 + 16 * h,
+                                  lambda b_=b_, rb=rb: e.valu(f"v_sub_f32 {b_}, {b_}, %[del{rb}]", b_, [b_]))
                         g.add(st, 4, rel1, 60 + 16 * h, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
                         if i & 1:
                             kk, j = 2 * h + (i >> 3), (i & 7) >> 1
@@ -1561,7 +1608,9 @@ class DqGen:
         for what, d in (("q", 68), ("o", 72)):
             for rb in range(2):
                 for ks in range(8):
-                    e.raw(f"buffer_load_dwordx4 %[{what}{rb * 8 + ks}], %[n{what}o{rb}], s[{d}:{d + 3}], 0 offen offset:{32 * ks}")
+                    # row block 1: 32 rows further (%[n{what}rs] = 32 row strides, as soffset)
+                    so = f"%[n{what}rs]" if rb else "0"
+                    e.raw(f"buffer_load_dwordx4 %[{what}{rb * 8 + ks}], %[n{what}o0], s[{d}:{d + 3}], {so} offen offset:{32 * ks}")
 
     # -- one unit (256 query rows), persistent across units -------------------------------------
     def build(self):
@@ -1588,6 +1637,20 @@ class DqGen:
         e.salu(f"s_mov_b32 {Q_PAR}, %[boff]")
         e.salu(f"s_add_i32 {Q_FIN}, %[ntiles], -1")
         e.salu(f"s_min_i32 {Q_NA}, %[na], {Q_FIN}")  # A chain: class A tiles before the final one
+        if self.dropout:
+            # keep words: tile 0's in %[mw*] (from the previous unit or the caller) -> both sets;
+            # period i requests tile i + 1's
+            e.salu("s_mov_b32 s92, %[mklo]")
+            e.salu("s_and_b32 s93, %[mkhi], 0xffff")
+            e.salu("s_mov_b32 s94, %[mkbytes]")
+            e.salu("s_mov_b32 s95, 0x20000")
+            e.salu(f"s_mov_b32 {Q_MOFF[0]}, 256")
+            e.salu(f"s_add_u32 {Q_MOFF[1]}, %[mrs], 256")
+            e.valu(f"v_mov_b32 {QMO}, %[mo0]", QMO)
+            for rb in range(2):
+                for h in range(2):
+                    for st in range(2):
+                        e.valu(f"v_mov_b32 {QMW(st, rb, h)}, %[mw{2 * rb + h}]", QMW(st, rb, h))
         # this unit's K(0), V(0) (requested by the previous unit or before the statement), Q, dO
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
@@ -1646,6 +1709,19 @@ class DqGen:
             self.period(par, "D")
             e.raw("s_branch .Lhp%=_loop")
         e.label(".Lhp%=_end")
+        if self.dropout:
+            # the final period requested the next unit's tile-0 words into set Q_PAR (flipped since)
+            e.raw(f"s_cmp_eq_u32 {Q_PAR}, 0")
+            e.raw("s_cbranch_scc0 .Lhp%=_mw1")
+            for st in range(2):
+                if st == 1:
+                    e.label(".Lhp%=_mw1")
+                for rb in range(2):
+                    for h in range(2):
+                        e.raw(f"v_mov_b32 %[mw{2 * rb + h}], {QMW(st, rb, h)}")
+                if st == 0:
+                    e.raw("s_branch .Lhp%=_mwd")
+            e.label(".Lhp%=_mwd")
         self.next_unit_loads()
         e.drain_lds()
         e.salu(f"s_mov_b32 m0, {SM0}")
@@ -1661,28 +1737,37 @@ class DqGen:
         e.salu(f"s_mov_b32 {SVP[1]}, %[nvhi]")
         e.salu(f"s_mov_b32 {SKR}, %[nkbytes]")
         e.salu(f"s_mov_b32 {SVR}, %[nkbytes]")
+        if self.dropout:  # the final period's keep words: the next unit's tile 0
+            e.valu(f"v_mov_b32 {QMO}, %[nmo0]", QMO)
+            e.salu(f"s_mov_b32 {Q_MOFF[0]}, 0")
+            e.salu(f"s_mov_b32 {Q_MOFF[1]}, %[mrs]")
 
 
-def gen_dq_function(bf16, causal):
-    g = DqGen(bf16, causal)
+def gen_dq_function(bf16, causal, dropout=False):
+    g = DqGen(bf16, causal, dropout)
     lines = g.build()
-    name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
-    clob = [f'"v{i}"' for i in range(DQ_NVGPR)] + [f'"a{i}"' for i in range(128)] + \
-           [f'"s{i}"' for i in SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
+    name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_drop' if dropout else ''}"
+    nv = DQ_NVGPR_DROP if dropout else DQ_NVGPR
+    sg = SGPR_CLOBBER + (list(range(92, 98)) if dropout else [])
+    clob = [f'"v{i}"' for i in range(nv)] + [f'"a{i}"' for i in range(128)] + \
+           [f'"s{i}"' for i in sg] + ['"vcc"', '"scc"', '"memory"']
     qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
     oops = ", ".join(f'[o{i}] "+a"(o[{i}])' for i in range(16))
+    mops = (",\n        " + ", ".join(f'[mw{i}] "+v"(mw[{i}])' for i in range(4))) if dropout else ""
     vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1",
-            "nqo0", "nqo1", "noo0", "noo1"]
+            "nqo0", "noo0"] + (["mo0", "nmo0", "msh"] if dropout else [])
     sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi", "sc",
-            "boff", "nklo", "nkhi", "nvlo", "nvhi", "nkbytes", "nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes"]
-    src = f"""// hand-placed dQ unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+            "boff", "nklo", "nkhi", "nvlo", "nvhi", "nkbytes", "nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes",
+            "nqrs", "nors"] + (["mklo", "mkhi", "mkbytes", "mrs", "dsc"] if dropout else [])
+    marg = ", uint32_t (&mw)[4]" if dropout else ""
+    src = f"""// hand-placed dQ unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}{', dropout' if dropout else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 // q / o: this unit's Q and dO fragments in, the NEXT unit's out -- still in flight (wait before
-// reading them)
-FA2_DEV void {name}(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a) {{
+// reading them){'; mw: the keep words of tile 0, in and (next unit) out' if dropout else ''}
+FA2_DEV void {name}(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a{marg}) {{
   asm volatile(
 {_asm_body(lines)}
       : {qops},
-        {oops}
+        {oops}{mops}
       : {", ".join(f'[{n}] "v"(a.{n})' for n in vops)},
         {", ".join(f'[{n}] "s"(a.{n})' for n in sops)}
       : {", ".join(clob)});
@@ -1730,6 +1815,13 @@ FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float
     return "".join(out)
 
 
+# Each read statement clobbers every accumulator register: a value live across them (the next
+# unit's Q / dO fragments, "+a" operands of the main statement) then cannot be placed in
+# a[0:127] anywhere between the main statement and the last read -- the compiler moving one
+# there early would overwrite accumulators not read yet (tests/test_code_objects.py checks the ISA).
+ACC_CLOBBER = ", ".join(f'"a{i}"' for i in range(128))
+
+
 def gen_read_o():
     parts = ["// O^T accumulators a[0:127] -> registers (after the main statement's final drain)",
              "FA2_DEV void fwd_hp_read_o(f32x16 (&o)[2][4]) {"]
@@ -1738,7 +1830,7 @@ def gen_read_o():
             base = (rb * 4 + dt) * 16
             outs = ", ".join(f'"=v"(o[{rb}][{dt}][{i}])' for i in range(16))
             body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
-            parts.append(f'  asm volatile("{body}" : {outs});')
+            parts.append(f'  asm volatile("{body}" : {outs} : : {ACC_CLOBBER});')
     parts.append("}")
     return "\n".join(parts) + "\n"
 
@@ -1764,7 +1856,8 @@ def write_headers():
     out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
     for bf16 in (True, False):
         for causal in (True, False):
-            out.append(gen_dq_function(bf16, causal))
+            for dropout in (False, True):
+                out.append(gen_dq_function(bf16, causal, dropout))
     out.append(gen_read_o().replace("fwd_hp_read_o", "dq_hp_read").replace("O^T accumulators", "dQ^T accumulators"))
     out.append("}  // namespace fa2\n")
     paths.append(_write(os.path.join(GEN, "dq_hp_body.h"), "\n".join(out)))

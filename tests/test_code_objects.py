@@ -121,6 +121,7 @@ def test_every_kernel_fits_the_cu(kernels):
 HP = {
     "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_fwd_args",
     "dkdv_hp": r"_ZN3fa214dkdv_hp_kernelILb[01]ELb[01]EEEv12fa2_bwd_argsi",
+    "dq_hp": r"_ZN3fa212dq_hp_kernelILb[01]ELb[01]ELb0EEEv12fa2_bwd_args",
 }
 
 
@@ -132,3 +133,52 @@ def test_hand_placed_kernels_have_no_scratch(kernels, kind):
     for k, (scratch, vgprs, lds) in found.items():
         assert scratch == 0, (k, scratch)
         assert vgprs <= 512 and lds <= 160 * 1024, (k, vgprs, lds)  # one workgroup of 4 waves per CU
+
+
+# The accumulators of a hand-placed kernel live in fixed AGPRs from the end of its main statement
+# until the read statements copy them out.  Nothing the compiler emits in between may write those
+# registers (a "+a" operand moved there early overwrote dQ rows once).  Checked on the ISA: from
+# the statement's closing `s_nop 15` pair to the last accumulator read, no AGPR write to them.
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+ACC_RANGE = {"fwd_hp": 128, "dq_hp": 128, "dkdv_hp": 256}
+
+
+def _disassemble(co: bytes, tmp_path, n):
+    import subprocess
+
+    f = tmp_path / f"co{n}.o"
+    f.write_bytes(co)
+    res = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(f)], capture_output=True, text=True)
+    return res.stdout
+
+
+@pytest.mark.parametrize("kind", sorted(ACC_RANGE))
+def test_accumulators_untouched_until_read(tmp_path, kind):
+    if not os.path.exists(_lib.LIB_PATH) or not os.path.exists(OBJDUMP):
+        pytest.skip("library or llvm-objdump missing")
+    n_acc = ACC_RANGE[kind]
+    sym = {"fwd_hp": "fwd_hp_kernel", "dq_hp": "dq_hp_kernel", "dkdv_hp": "dkdv_hp_kernel"}[kind]
+    checked = 0
+    for n, co in enumerate(_code_objects(_lib.LIB_PATH)):
+        if sym.encode() not in co:
+            continue
+        text = _disassemble(co, tmp_path, n)
+        for func in re.split(r"\n(?=[0-9a-f]+ <)", text):
+            if sym not in func.split("\n", 1)[0]:
+                continue
+            lines = [ln.split("//")[0].strip() for ln in func.split("\n")[1:]]
+            lines = [ln for ln in lines if ln]
+            i = 0
+            while i < len(lines):
+                if lines[i].startswith("s_nop 15") and i + 1 < len(lines) and lines[i + 1].startswith("s_nop 15"):
+                    # window: up to the read of the last accumulator register
+                    last = f"a{n_acc - 1}"
+                    j = i + 2
+                    while j < len(lines) and not (lines[j].startswith("v_accvgpr_read_b32") and lines[j].endswith(last)):
+                        m = re.match(r"(v_accvgpr_write_b32|v_accvgpr_mov_b32|\w*load\w*)\s+a\[?(\d+)", lines[j])
+                        assert not (m and int(m.group(2)) < n_acc), (kind, lines[j])
+                        j += 1
+                    checked += 1
+                    i = j
+                i += 1
+    assert checked > 0, f"no {kind} main statement found"
