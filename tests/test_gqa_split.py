@@ -86,10 +86,12 @@ def test_split_matches_oracle(b, hq, hkv, sq, sk, d, causal, p, mask, bias, dtyp
 
 
 @pytest.mark.gpu
-@pytest.mark.xfail(strict=True, reason="bf16 MQA Sq=Sk=777 causal: the largest dV element rounds to -16.625 "
-                   "where the fp32 oracle gives -16.5, one bf16 ulp over the reference rule, with and without "
-                   "the q-head split alike (bit-identical dV: one q-head per split sums in the same order; "
-                   "scripts/diag_split.py).  Kept visible rather than switched to fp16 (ADVICE r02).")
+@pytest.mark.xfail(strict=True, reason="bf16 MQA Sq=Sk=777 causal, dV[0, 105]: the fp32 oracle is -16.5664 (bf16 "
+                   "-16.625), this library -16.5; an fp32 sum with P rounded to bf16 first -- the MFMA operand "
+                   "here and in the reference's own dV (tl.dot(tl.trans(p).to(do.dtype), do), "
+                   "src/backward/compute_dkdv.py:100) -- gives -16.5579 (bf16 -16.5): the 12432-term sum sits "
+                   "0.004 from the -16.5625 rounding boundary and the bf16 quantisation of P moves it across.  "
+                   "The rule's PyTorch baseline keeps P in fp32 and rounds like the oracle (scripts/diag_xfail.py).")
 def test_split_mqa_777_causal_bf16():
     run_case(1, 16, 1, 777, 777, 128, True, 0.0, False, False, torch.bfloat16, forward_only=False)
 
