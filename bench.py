@@ -57,6 +57,10 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PEAK_TFLOPS = 2500.0  # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+# Philox4x32-10 draws per second over the whole chip (bench_micro/philox_rate.hip, the library's
+# philox_uniform at full occupancy; profiles/r04g_philox_rate.txt): the VALU bound of the dropout
+# forward, which draws one uniform per visible (row, key) as the reference's tl.rand does
+PHILOX_DRAWS_PER_S = 8.9158e11
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md: ~8 TB/s)
 N_SIMDS = 1024  # 256 CUs x 4 SIMDs
 METRIC = "attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16; % of MFMA peak"
@@ -596,6 +600,16 @@ def main():
     }
     if not fwd_only:
         line["roofline_dq"] = roofline("dq_kernel")
+    if p_drop > 0:
+        # visible (row, key) pairs of one forward launch: one Philox draw each
+        vis = s * (s + 1) // 2 if causal else s * s
+        draws = b * h * vis
+        rate = draws / t_fwd
+        line["roofline_valu"] = {"bound": "valu", "kernel": "fa2::fwd_kernel", "achieved": round(rate, 1),
+                                 "peak": PHILOX_DRAWS_PER_S, "unit": "Philox draws/s",
+                                 "frac": round(rate / PHILOX_DRAWS_PER_S, 4), "draws_per_launch": draws,
+                                 "bound_ms": round(draws / PHILOX_DRAWS_PER_S * 1e3, 4),
+                                 "peak_source": "bench_micro/philox_rate.hip (profiles/r04g_philox_rate.txt)"}
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

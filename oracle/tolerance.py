@@ -46,6 +46,13 @@ def within_one_ulp(x: Tensor, ref: Tensor) -> bool:
     return bool(((x.float() - r).abs() <= ulp).all().item())
 
 
+# How often each escape beyond the reference's rule decided a check (reported by tests/conftest.py
+# at the end of a run, so the 1-ulp branch cannot widen silently): "ulp" = err > mul * err_pt +
+# bias accepted only because err_pt == 0 and every element is within one ulp; "dv_sum" = the
+# reference's own small-dV-sum escape (tests/utils.py of the reference).
+ESCAPES = {"checks": 0, "ulp": 0, "dv_sum": 0}
+
+
 def check_fa_tolerance(
     q: Tensor,
     k: Tensor,
@@ -63,8 +70,11 @@ def check_fa_tolerance(
     """Raise AssertionError when the rule above is violated; return the measured errors."""
     report = {"out": _maxdiff(out, out_ref), "out_pt": _maxdiff(out_pt, out_ref)}
     report["out_rtol"] = _rtol(report["out"], out_ref)
-    assert report["out"] <= out_error_mul * report["out_pt"] + out_error_bias or (
-        report["out_pt"] == 0 and within_one_ulp(out, out_ref)), f"Output {report}"
+    ESCAPES["checks"] += 1
+    rule = report["out"] <= out_error_mul * report["out_pt"] + out_error_bias
+    ulp = not rule and report["out_pt"] == 0 and within_one_ulp(out, out_ref)
+    ESCAPES["ulp"] += int(ulp)
+    assert rule or ulp, f"Output {report}"
     if do is None:
         return report
     if grads is None:
@@ -75,11 +85,16 @@ def check_fa_tolerance(
         err, err_pt = _maxdiff(g, gr), _maxdiff(gp, gr)
         report[name], report[name + "_pt"] = err, err_pt
         report[name + "_rtol"] = _rtol(err, gr)
-        ok = err <= grad_error_mul * err_pt + grad_error_bias or (err_pt == 0 and within_one_ulp(g, gr))
+        ESCAPES["checks"] += 1
+        ok = err <= grad_error_mul * err_pt + grad_error_bias
+        if not ok and err_pt == 0 and within_one_ulp(g, gr):
+            ESCAPES["ulp"] += 1
+            ok = True
         if not ok and name == "dv":
             total = (g.float() - gr.float()).abs().sum().item()
             if total < 1e-4:
                 warnings.warn(f"small dV errors summing to {total}", stacklevel=2)
+                ESCAPES["dv_sum"] += 1
                 ok = True
         assert ok, f"Gradient of {name}: {report}"
     return report
