@@ -1159,108 +1159,177 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 // Bias gradient (ABI 5; the reference has none, /root/reference/src/wrapper.py:86):
 //   dbias[b', h', i, j] = sum over the (batch, q-head) pairs the bias broadcasts to of
 //                         dS[b, hq, i, j] = P (dP~ - delta),   P = exp2(s scale log2e + bias log2e - LSE2)
-// (dP~ = dP M / (1 - p) under dropout, M the forward's keep mask), in fp32, deterministic: one
-// workgroup owns 128 rows of one bias slice (b', h') and adds the pairs of its broadcast group one
-// after the other into those rows (the first pair stores, the next ones read-add-store their own
-// earlier writes), so the memory is the bias-shaped output alone -- no [B, Hq, Sq, Sk] buffer.
-// The workgroup's keys are a chunk of kDbiasChunk tiles, so that a broadcast bias still spreads
-// over (Sq / 128) x (Sk / 512) workgroups per slice.
+// (dP~ = dP M / (1 - p) under dropout, M the forward's keep mask), in fp32, deterministic.
+// One workgroup owns a 128-row x (64 kDbiasChunk)-key block of one bias slice (b', h') and sums
+// the pairs of its broadcast group into registers, pair after pair in index order, then stores
+// the block once: no read-modify-write of the output, and the memory is the bias-shaped output
+// alone -- no [B, Hq, Sq, Sk] buffer.  The bias values are the same for every pair of the group
+// (the summed dimensions have stride 0), so the block's bias is read once, into registers.
 // Per pair the structure is dq_kernel's (query on the lane, Q / dO in registers, 64-key K/V tiles
 // in LDS): S^T = K Q^T and dP^T = V dO^T (the same products as compute_dq.py:38-69), without the
-// dQ GEMM.  delta comes from the dQ (or delta) kernel that ran before (-rowsum(O dO), negated).
-constexpr int kDbiasChunk = 8;  // 64-key tiles per dbias workgroup
+// dQ GEMM; the next K/V tile and the next pair's Q/dO rows stream into LDS while the current
+// pair computes.
+// delta comes from the dQ (or delta) kernel that ran before (-rowsum(O dO), negated).
+constexpr int kDbiasChunk = 2;  // 64-key tiles per dbias workgroup
+
+// XCD-aware block order: workgroup g runs on XCD g % 8 as that XCD's (g / 8)-th; the blocks go
+// out in 8 x 8 squares of (row block, key chunk), square s to XCD s % 8, so the workgroups an XCD
+// runs together share 8 row blocks' Q / dO and 8 key chunks' K / V in its L2 (each read by 8
+// workgroups instead of 1) and the causal triangle's squares spread evenly over the XCDs.
+// The grid is padded to whole squares per XCD (dbias_grid); padding workgroups get mb = -1.
+constexpr int kDbiasSq = 8;
+__host__ __device__ inline int dbias_squares(int nmb, int nkc) {
+  const int sq = ((nmb + kDbiasSq - 1) / kDbiasSq) * ((nkc + kDbiasSq - 1) / kDbiasSq);
+  return (sq + 7) / 8 * 8;
+}
+FA2_DEV void dbias_block(int g, int nmb, int nkc, int& mb, int& kc) {
+  const int x = g & 7, j = g >> 3;
+  const int s = (j / (kDbiasSq * kDbiasSq)) * 8 + x, within = j % (kDbiasSq * kDbiasSq);
+  const int sqk = (nkc + kDbiasSq - 1) / kDbiasSq;
+  mb = (s / sqk) * kDbiasSq + within / kDbiasSq;
+  kc = (s % sqk) * kDbiasSq + within % kDbiasSq;
+  if (mb >= nmb || kc >= nkc) mb = -1;
+}
 
 template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
-__global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
-  constexpr int NT = 256, BM = 128, BN = 64;
+  constexpr int NT = 256, BM = 128, BN = 64, C = kDbiasChunk;
   constexpr int KS = DT / 16;
   constexpr int TILE = BN * DT * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];
+  // D <= 128: the pair's Q / dO rows go through LDS (coalesced 16-byte DMA pieces, then one
+  // fragment read per lane): loaded straight into the row-per-lane registers, every load
+  // instruction would touch 32 rows x 32 bytes and the address unit, not the MFMAs, would set
+  // the pace.  D = 256 loads them into registers directly (the LDS would not hold both tiles).
+  constexpr bool QLDS = DT <= 128;
+  constexpr int QTILE = QLDS ? BM * DT * 2 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + 2 * QTILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int nkt = (p.seqlen_k + BN - 1) / BN;        // key tiles of the output rows
-  const int nkc = (nkt + kDbiasChunk - 1) / kDbiasChunk;
-  const int mb = blockIdx.x / nkc, kc = blockIdx.x - mb * nkc;
-  const int t0 = kc * kDbiasChunk, t1 = min(nkt, t0 + kDbiasChunk);  // this workgroup's key tiles
+  const int nkc = (nkt + C - 1) / C;
+  int mb, kc;
+  dbias_block(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, mb, kc);
+  if (mb < 0) return;                                // grid padding
+  const int t0 = kc * C, t1 = min(nkt, t0 + C);     // this workgroup's key tiles
   const int Hb = p.bias_stride[1] != 0 ? p.heads_q : 1;
   const int slice = blockIdx.y;                       // (b', h') of the bias
   const int bb = slice / Hb, hb = slice - bb * Hb;
   const bool sum_b = p.bias_stride[0] == 0, sum_h = p.bias_stride[1] == 0;
   const int nb = sum_b ? p.batch : 1, nh = sum_h ? p.heads_q : 1;
+  const int np = nb * nh;
   const int D = p.head_dim;
-  const int mw0 = mb * BM + 32 * w;
-  const int qi = mw0 + r32;                          // this lane's row
+  const int m0 = mb * BM;
+  const int qi = m0 + 32 * w + r32;                  // this lane's row
   const float scale2 = p.softmax_scale * kLog2e;
-  float* drow = p.dbias + bb * p.dbias_stride[0] + hb * p.dbias_stride[1] + (int64_t)(qi < p.seqlen_q ? qi : 0) * p.dbias_stride[2];
   const bool row_in = qi < p.seqlen_q;
 
   auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
   auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
+  char* const qt = smem + 4 * TILE;
+  char* const ot = smem + 4 * TILE + QTILE;
   BufStager<DT, BN, NT> kst;
-  int mrows = 0;
+  BufStager<DT, BM, NT> qst, ost;
+  int mrows = 0, qrows = 0, orows = 0;
   if (ALIGNED) {
     kst.init(tid, p.k_stride[1], D);
     mrows = BufStager<DT, BN, NT>::max_rows(p.k_stride[1]);
+    if (QLDS) {
+      qst.init(tid, p.q_stride[1], D);
+      ost.init(tid, p.do_stride[1], D);
+      qrows = BufStager<DT, BM, NT>::max_rows(p.q_stride[1]);
+      orows = BufStager<DT, BM, NT>::max_rows(p.do_stride[1]);
+    }
   }
 
-  // sixteen dS values of this lane for keys n0 + 32 t + 8 g + 4 hh + (0..3), g = 0..3, into the
-  // output row: the first pair stores, later pairs add to what this lane stored before
-  // (16-byte accesses when the rows allow them: the 4 keys of a group are contiguous)
-  const bool vec4 = ((uintptr_t)p.dbias & 15) == 0 && p.dbias_stride[0] % 4 == 0 && p.dbias_stride[1] % 4 == 0 &&
-                    p.dbias_stride[2] % 4 == 0;
-  auto emit = [&](const f32x16& ds, int n0, int t, bool first) {
-    if (!row_in) return;
+  // element i of half t of tile c: key (t0 + c) 64 + 32 t + 8 (i / 4) + 4 hh + i % 4
+  float acc[C][2][16], bl[C][2][16];
+  {
+    const int64_t brow = bb * p.bias_stride[0] + hb * p.bias_stride[1] + (int64_t)(row_in ? qi : 0) * p.bias_stride[2];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int k0 = n0 + 32 * t + 8 * g + 4 * hh;
-      if (vec4 && k0 + 4 <= p.seqlen_k) {
-        f32x4 v = {ds[4 * g], ds[4 * g + 1], ds[4 * g + 2], ds[4 * g + 3]};
-        if (!first) v += *(const f32x4*)(drow + k0);
-        *(f32x4*)(drow + k0) = v;
-      } else {
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (k0 + j < p.seqlen_k) {
-            const float v = ds[4 * g + j];
-            drow[k0 + j] = first ? v : drow[k0 + j] + v;
-          }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kj = (t0 + c) * BN + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          acc[c][t][i] = 0.f;
+          bl[c][t][i] = kLog2e * load_bias(p.bias, brow + (kj < p.seqlen_k ? kj : p.seqlen_k - 1), p.bias_dtype);
         }
+  }
+
+  // the pair's visible key tiles are [t0, tend); a pair with none adds nothing
+  struct Pair {
+    int b, hq, Lq, Lk, tend;
+  };
+  auto pair_at = [&](int pair) {
+    Pair r;
+    r.b = sum_b ? pair / nh : bb;
+    r.hq = sum_h ? (sum_b ? pair - (pair / nh) * nh : pair) : hb;
+    r.Lq = p.seqlen_q;
+    r.Lk = p.seqlen_k;
+    if (p.cu_seqlens) r.Lq = r.Lk = p.cu_seqlens[r.b + 1] - p.cu_seqlens[r.b];
+    int n_end = 0;
+    if (m0 < r.Lq) n_end = max(CAUSAL ? min(r.Lk, m0 + BM + r.Lk - r.Lq) : r.Lk, 0);
+    r.tend = min(t1, (n_end + BN - 1) / BN);
+    return r;
+  };
+  auto next_visible = [&](int pair) {
+    while (pair < np && pair_at(pair).tend <= t0) ++pair;
+    return pair;
+  };
+  auto stage_kv = [&](int buf, const Pair& r, int n) {
+    const int hkv = r.hq / (p.heads_q / p.heads_kv);
+    const uint16_t* kg = (const uint16_t*)p.k + r.b * p.k_stride[0] + hkv * p.k_stride[2];
+    const uint16_t* vg = (const uint16_t*)p.v + r.b * p.v_stride[0] + hkv * p.v_stride[2];
+    if constexpr (ALIGNED) {
+      kst.issue(kt(buf), kg, p.k_stride[1], n, r.Lk, mrows);
+      kst.issue(vt(buf), vg, p.v_stride[1], n, r.Lk, mrows);
+    } else {
+      stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, r.Lk, D, tid);
+      stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, r.Lk, D, tid);
+    }
+  };
+  auto q_base = [&](const Pair& r) { return (const uint16_t*)p.q + r.b * p.q_stride[0] + r.hq * p.q_stride[2]; };
+  auto o_base = [&](const Pair& r) { return (const uint16_t*)p.dout + r.b * p.do_stride[0] + r.hq * p.do_stride[2]; };
+  auto stage_qo = [&](const Pair& r) {  // the pair's 128 Q / dO rows of this block into LDS
+    if constexpr (QLDS) {
+      if constexpr (ALIGNED) {
+        qst.issue(qt, q_base(r), p.q_stride[1], m0, r.Lq, qrows);
+        ost.issue(ot, o_base(r), p.do_stride[1], m0, r.Lq, orows);
+      } else {
+        stage_tile<DT, BM, NT, false>(qt, q_base(r), p.q_stride[1], m0, r.Lq, D, tid);
+        stage_tile<DT, BM, NT, false>(ot, o_base(r), p.do_stride[1], m0, r.Lq, D, tid);
       }
     }
   };
 
-  for (int pair = 0; pair < nb * nh; ++pair) {
-    const int b = sum_b ? pair / nh : bb;
-    const int hq = sum_h ? (sum_b ? pair - (pair / nh) * nh : pair) : hb;
-    const bool first = pair == 0;
-    const int hkv = hq / (p.heads_q / p.heads_kv);
-    int Lq = p.seqlen_q, Lk = p.seqlen_k;
-    if (p.cu_seqlens) Lq = Lk = p.cu_seqlens[b + 1] - p.cu_seqlens[b];
-    const int diag = Lk - Lq;
-    const int m0 = mb * BM;
-    int n_end = 0;
-    if (m0 < Lq) n_end = max(CAUSAL ? min(Lk, m0 + BM + diag) : Lk, 0);
-    const int tend = min(t1, (n_end + BN - 1) / BN);  // tiles [t0, tend) hold visible pairs
-    const uint16_t* kg = (const uint16_t*)p.k + b * p.k_stride[0] + hkv * p.k_stride[2];
-    const uint16_t* vg = (const uint16_t*)p.v + b * p.v_stride[0] + hkv * p.v_stride[2];
-    auto stage_kv = [&](int buf, int n) {
-      if constexpr (ALIGNED) {
-        kst.issue(kt(buf), kg, p.k_stride[1], n, Lk, mrows);
-        kst.issue(vt(buf), vg, p.v_stride[1], n, Lk, mrows);
-      } else {
-        stage_tile<DT, BN, NT, false>(kt(buf), kg, p.k_stride[1], n, Lk, D, tid);
-        stage_tile<DT, BN, NT, false>(vt(buf), vg, p.v_stride[1], n, Lk, D, tid);
-      }
-    };
-    if (tend > t0) stage_kv(0, t0 * BN);
+  int pair = next_visible(0);
+  int buf = 0;
+  if (pair < np) {
+    const Pair r = pair_at(pair);
+    stage_kv(0, r, t0 * BN);
+    stage_qo(r);
+  }
+  vm_wait_all();
+  __syncthreads();
+  while (pair < np) {
+    const Pair r = pair_at(pair);
+    const int nxt = next_visible(pair + 1);
+    const int b = r.b, hq = r.hq, Lq = r.Lq, Lk = r.Lk;
     const bool qvalid = qi < Lq;
     u32x4 qf[KS], of[KS];
-    {
-      const uint16_t* qrow = (const uint16_t*)p.q + b * p.q_stride[0] + hq * p.q_stride[2] + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
-      const uint16_t* orow = (const uint16_t*)p.dout + b * p.do_stride[0] + hq * p.do_stride[2] + (int64_t)(qvalid ? qi : 0) * p.do_stride[1];
+    if constexpr (QLDS) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        qf[ks] = lds_row_frag<DT, BM>(qt, 32 * w, r32, ks, hh);
+        of[ks] = lds_row_frag<DT, BM>(ot, 32 * w, r32, ks, hh);
+      }
+    } else {
+      const uint16_t* qrow = q_base(r) + (int64_t)(qvalid ? qi : 0) * p.q_stride[1];
+      const uint16_t* orow = o_base(r) + (int64_t)(qvalid ? qi : 0) * p.do_stride[1];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         qf[ks] = load_row_frag<ALIGNED>(qrow, 16 * ks + 8 * hh, D, qvalid);
@@ -1270,7 +1339,13 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2
     const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride;
     const float nlse = qvalid ? -p.lse[srow + qi] : 0.f;
     const float ndel = qvalid ? p.delta[srow + qi] : 0.f;  // the workspace holds -delta
-    const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + diag + 1) : Lk);
+    if constexpr (QLDS) {
+      // every wave holds its fragments: the next pair's rows may overwrite the tiles
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __syncthreads();
+      if (nxt < np) stage_qo(pair_at(nxt));
+    }
+    const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + Lk - Lq + 1) : Lk);
     uint64_t drop_row = 0;
     float inv_keep = 1.f;
     if (DROPOUT) {
@@ -1279,61 +1354,74 @@ __global__ void __launch_bounds__(256, DT >= 256 ? 1 : 2) dbias_kernel(const fa2
                  (uint64_t)qi * (uint64_t)Lk;
       inv_keep = 1.f / (1.f - p.dropout_p);
     }
-    const void* biasb = p.bias;
-    const int64_t bias_row = b * p.bias_stride[0] + hq * p.bias_stride[1] + (int64_t)(qvalid ? qi : 0) * p.bias_stride[2];
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
 
-    for (int it = t0; it < tend; ++it) {
-      const int cur = (it - t0) & 1;
-      const int n0 = it * BN;
-      if (it + 1 < tend) stage_kv(cur ^ 1, n0 + BN);
-      const char* K = kt(cur);
-      const char* V = vt(cur);
-      const int rel = lim_lane - n0 - 4 * hh;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        uint32_t mwd = 0u;  // the forward's saved keep word of this row and key half
-        if (DROPOUT && p.dropout_mask && qvalid && n0 + 32 * t < p.seqlen_k) {
-          const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
-          mwd = p.dropout_mask[((((int64_t)(b * p.heads_q + hq) * nrb + (qi >> 5)) * ncw + ((n0 >> 5) + t)) * 32) + (qi & 31)];
-        }
-        f32x16 s = zero16(), dp = zero16();
+    for (int c = 0; c < C; ++c) {
+      const int it = t0 + c;
+      if (it < r.tend) {
+        const int n0 = it * BN;
+        // the next tile: this pair's, else the next visible pair's first
+        if (it + 1 < r.tend) stage_kv(buf ^ 1, r, n0 + BN);
+        else if (nxt < np) stage_kv(buf ^ 1, pair_at(nxt), t0 * BN);
+        const char* K = kt(buf);
+        const char* V = vt(buf);
+        const int rel = lim_lane - n0 - 4 * hh;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
-          dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
-        }
-        f32x16 ds;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int o = 32 * t + (i & 3) + 8 * (i >> 2);
-          const int kj = n0 + o + 4 * hh;
-          const int kc = kj < Lk ? kj : Lk - 1;
-          const float x = fmaf(s[i], scale2, kLog2e * load_bias(biasb, bias_row + kc, p.bias_dtype));
-          float pr = __builtin_amdgcn_exp2f(x + nlse);
-          pr = o < rel ? pr : 0.f;
-          float dpv = dp[i];
-          if (DROPOUT) {
-            const bool keep = p.dropout_mask ? ((mwd >> ((i & 3) + 8 * (i >> 2) + 4 * hh)) & 1u) != 0
-                                             : philox_uniform(p.dropout_seed, drop_row + (uint64_t)kj) > p.dropout_p;
-            dpv *= keep ? inv_keep : 0.f;
+        for (int t = 0; t < 2; ++t) {
+          uint32_t mwd = 0u;  // the forward's saved keep word of this row and key half
+          if (DROPOUT && p.dropout_mask && qvalid && n0 + 32 * t < p.seqlen_k) {
+            const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+            mwd = p.dropout_mask[((((int64_t)(b * p.heads_q + hq) * nrb + (qi >> 5)) * ncw + ((n0 >> 5) + t)) * 32) + (qi & 31)];
           }
-          ds[i] = pr * (dpv + ndel);
+          f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
+            dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int o = 32 * t + (i & 3) + 8 * (i >> 2);
+            float pr = __builtin_amdgcn_exp2f(fmaf(s[i], scale2, bl[c][t][i]) + nlse);
+            pr = o < rel ? pr : 0.f;
+            float dpv = dp[i];
+            if (DROPOUT) {
+              const bool keep = p.dropout_mask ? ((mwd >> ((i & 3) + 8 * (i >> 2) + 4 * hh)) & 1u) != 0
+                                               : philox_uniform(p.dropout_seed, drop_row + (uint64_t)(n0 + o + 4 * hh)) > p.dropout_p;
+              dpv *= keep ? inv_keep : 0.f;
+            }
+            acc[c][t][i] += pr * (dpv + ndel);
+          }
         }
-        emit(ds, n0, t, first);
-      }
-      vm_wait_all();
-      __syncthreads();
-    }
-    if (first) {  // key tiles this pair does not see: zeros, so that later pairs can add
-      const f32x16 z = zero16();
-      for (int it = max(tend, t0); it < t1; ++it) {
-        emit(z, it * BN, 0, true);
-        emit(z, it * BN, 1, true);
+        vm_wait_all();
+        __syncthreads();
+        buf ^= 1;
       }
     }
-    vm_wait_all();
+    pair = nxt;
+  }
+
+  // one store of the block (16-byte stores when the rows allow them: a group's 4 keys are contiguous)
+  if (!row_in) return;
+  float* drow = p.dbias + bb * p.dbias_stride[0] + hb * p.dbias_stride[1] + (int64_t)qi * p.dbias_stride[2];
+  const bool vec4 = ((uintptr_t)p.dbias & 15) == 0 && p.dbias_stride[0] % 4 == 0 && p.dbias_stride[1] % 4 == 0 &&
+                    p.dbias_stride[2] % 4 == 0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (t0 + c >= t1) break;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = (t0 + c) * BN + 32 * t + 8 * g + 4 * hh;
+        if (vec4 && k0 + 4 <= p.seqlen_k) {
+          *(f32x4*)(drow + k0) = f32x4{acc[c][t][4 * g], acc[c][t][4 * g + 1], acc[c][t][4 * g + 2], acc[c][t][4 * g + 3]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (k0 + j < p.seqlen_k) drow[k0 + j] = acc[c][t][4 * g + j];
+        }
+      }
   }
 }
 
@@ -1393,7 +1481,7 @@ dq_done:
   if ((stages & 8) && BIAS && a.dbias && a.seqlen_q > 0 && a.seqlen_k > 0) {
     const int bb = a.bias_stride[0] != 0 ? a.batch : 1, hb = a.bias_stride[1] != 0 ? a.heads_q : 1;
     const int nkc = ((a.seqlen_k + 63) / 64 + kDbiasChunk - 1) / kDbiasChunk;
-    dim3 grid(((a.seqlen_q + 127) / 128) * nkc, bb * hb);
+    dim3 grid(dbias_squares((a.seqlen_q + 127) / 128, nkc) * kDbiasSq * kDbiasSq, bb * hb);
     hipLaunchKernelGGL((dbias_kernel<BF16, DT, CAUSAL, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if ((stages & 2) && a.seqlen_k > 0) {
