@@ -1173,22 +1173,29 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 constexpr int kDbiasChunk = 2;  // 64-key tiles per dbias workgroup
 
 // XCD-aware block order: workgroup g runs on XCD g % 8 as that XCD's (g / 8)-th; the blocks go
-// out in 8 x 8 squares of (row block, key chunk), square s to XCD s % 8, so the workgroups an XCD
-// runs together share 8 row blocks' Q / dO and 8 key chunks' K / V in its L2 (each read by 8
-// workgroups instead of 1) and the causal triangle's squares spread evenly over the XCDs.
-// The grid is padded to whole squares per XCD (dbias_grid); padding workgroups get mb = -1.
-constexpr int kDbiasSq = 8;
-__host__ __device__ inline int dbias_squares(int nmb, int nkc) {
-  const int sq = ((nmb + kDbiasSq - 1) / kDbiasSq) * ((nkc + kDbiasSq - 1) / kDbiasSq);
-  return (sq + 7) / 8 * 8;
+// out in 8 x 8 squares of (row block, key chunk), so the workgroups an XCD runs together share
+// 8 row blocks' Q / dO and 8 key chunks' K / V in its L2 (each read by 8 workgroups instead of
+// 1).  Square (r, c) goes to XCD (r + c) % 8: anti-diagonals, so that the causal triangle's
+// squares spread evenly over the XCDs (square columns would give XCD 0 fifteen times XCD 7's
+// work).  The square columns are padded to a multiple of 8 (dbias_blocks); padding
+// workgroups get mb = -1.
+// (grids under 32 x 32 blocks use 1 x 1 "squares": whole squares would crowd them onto few XCDs)
+__host__ __device__ inline int dbias_side(int nmb, int nkc) { return nmb >= 32 && nkc >= 32 ? 8 : 1; }
+__host__ __device__ inline int dbias_blocks(int nmb, int nkc) {  // the padded grid
+  const int e = dbias_side(nmb, nkc);
+  const int sqr = (nmb + e - 1) / e, sqk = (nkc + e - 1) / e;
+  return sqr * ((sqk + 7) / 8 * 8) * e * e;
 }
 FA2_DEV void dbias_block(int g, int nmb, int nkc, int& mb, int& kc) {
+  const int e = dbias_side(nmb, nkc);
   const int x = g & 7, j = g >> 3;
-  const int s = (j / (kDbiasSq * kDbiasSq)) * 8 + x, within = j % (kDbiasSq * kDbiasSq);
-  const int sqk = (nkc + kDbiasSq - 1) / kDbiasSq;
-  mb = (s / sqk) * kDbiasSq + within / kDbiasSq;
-  kc = (s % sqk) * kDbiasSq + within % kDbiasSq;
-  if (mb >= nmb || kc >= nkc) mb = -1;
+  const int q = j / (e * e), within = j % (e * e);
+  const int sqk = (nkc + e - 1) / e, per_row = (sqk + 7) / 8;
+  const int r = q / per_row, m = q - r * per_row;
+  const int c = ((x - r) & 7) + 8 * m;  // (r + c) % 8 == x
+  mb = r * e + within / e;
+  kc = c * e + within % e;
+  if (c >= sqk || mb >= nmb || kc >= nkc) mb = -1;
 }
 
 template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
@@ -1203,7 +1210,13 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
   // the pace.  D = 256 loads them into registers directly (the LDS would not hold both tiles).
   constexpr bool QLDS = DT <= 128;
   constexpr int QTILE = QLDS ? BM * DT * 2 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + 2 * QTILE];
+  // K/V tiles: a ring of 3 (D <= 128; staged two steps ahead) or 2 (D = 256, one step ahead)
+  constexpr int RING = QLDS ? 3 : 2;
+  // the deep pipeline counts its loads: fixed VMEM instructions per step (LDS-DMA pieces per
+  // K/V tile and per Q/dO block, plus the two -LSE / -delta loads), then "all but this step's"
+  constexpr int KV_VM = 2 * BufStager<DT, BN, NT>::kIters, QO_VM = 2 * BufStager<DT, BM, NT>::kIters + 2;
+  constexpr bool DEEP = QLDS && ALIGNED && !DROPOUT && C == 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * RING * TILE + 2 * QTILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1228,8 +1241,8 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
 
   auto kt = [&](int buf) { return smem + buf * 2 * TILE; };
   auto vt = [&](int buf) { return smem + TILE + buf * 2 * TILE; };
-  char* const qt = smem + 4 * TILE;
-  char* const ot = smem + 4 * TILE + QTILE;
+  char* const qt = smem + 2 * RING * TILE;
+  char* const ot = smem + 2 * RING * TILE + QTILE;
   BufStager<DT, BN, NT> kst;
   BufStager<DT, BM, NT> qst, ost;
   int mrows = 0, qrows = 0, orows = 0;
@@ -1308,10 +1321,22 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
 
   int pair = next_visible(0);
   int buf = 0;
+  // staging cursor (pair, tile) of the K/V ring, RING - 1 steps ahead of the compute; past the
+  // last pair it re-stages a tile of the current pair (unused) so every step issues the same loads
+  int spair = pair, sc = 0;
+  auto advance = [&]() {
+    if (++sc == C) {
+      sc = 0;
+      spair = next_visible(spair + 1);
+    }
+  };
   if (pair < np) {
     const Pair r = pair_at(pair);
-    stage_kv(0, r, t0 * BN);
     stage_qo(r);
+    for (int k = 0; k < RING - 1; ++k) {
+      stage_kv(k, spair < np ? pair_at(spair) : r, t0 * BN + (spair < np ? sc : 0) * BN);
+      advance();
+    }
   }
   vm_wait_all();
   __syncthreads();
@@ -1337,13 +1362,16 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
       }
     }
     const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride;
-    const float nlse = qvalid ? -p.lse[srow + qi] : 0.f;
-    const float ndel = qvalid ? p.delta[srow + qi] : 0.f;  // the workspace holds -delta
+    // (unconditional loads, so that the step's VMEM count is fixed; row 0 exists: Lq > 0)
+    const float lse_v = p.lse[srow + (qvalid ? qi : 0)], del_v = p.delta[srow + (qvalid ? qi : 0)];
+    const float nlse = qvalid ? -lse_v : 0.f;
+    const float ndel = qvalid ? del_v : 0.f;  // the workspace holds -delta
     if constexpr (QLDS) {
       // every wave holds its fragments: the next pair's rows may overwrite the tiles
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __syncthreads();
       if (nxt < np) stage_qo(pair_at(nxt));
+      else if (DEEP) stage_qo(r);  // (unused: keeps the step's load count)
     }
     const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + Lk - Lq + 1) : Lk);
     uint64_t drop_row = 0;
@@ -1358,16 +1386,21 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const int it = t0 + c;
-      if (it < r.tend) {
+      if (RING == 3 || it < r.tend) {
         const int n0 = it * BN;
-        // the next tile: this pair's, else the next visible pair's first
-        if (it + 1 < r.tend) stage_kv(buf ^ 1, r, n0 + BN);
-        else if (nxt < np) stage_kv(buf ^ 1, pair_at(nxt), t0 * BN);
+        if constexpr (RING == 3) {  // the tile RING - 1 steps ahead (every step of a pair runs)
+          stage_kv(buf == 0 ? 2 : buf - 1, spair < np ? pair_at(spair) : r, (t0 + (spair < np ? sc : 0)) * BN);
+          advance();
+        } else {  // the next tile: this pair's, else the next visible pair's first
+          if (it + 1 < r.tend) stage_kv(buf ^ 1, r, n0 + BN);
+          else if (nxt < np) stage_kv(buf ^ 1, pair_at(nxt), t0 * BN);
+        }
         const char* K = kt(buf);
         const char* V = vt(buf);
         const int rel = lim_lane - n0 - 4 * hh;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
+          if (it >= r.tend) break;  // a ring step over a tile this pair does not see
           uint32_t mwd = 0u;  // the forward's saved keep word of this row and key half
           if (DROPOUT && p.dropout_mask && qvalid && n0 + 32 * t < p.seqlen_k) {
             const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
@@ -1393,9 +1426,20 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
             acc[c][t][i] += pr * (dpv + ndel);
           }
         }
-        vm_wait_all();
+        if constexpr (DEEP) {
+          // everything but this step's loads: the next step's tile (and, at a pair's end, the
+          // next pair's Q / dO) has landed; s_waitcnt vmcnt(n): bits 3:0 and 15:14 of the count
+          static_assert(KV_VM + QO_VM < 64, "vmcnt range");
+          constexpr int n0c = KV_VM + QO_VM, n1c = KV_VM;
+          if (c == 0)
+            __builtin_amdgcn_s_waitcnt((n0c & 15) | ((n0c >> 4) << 14) | 0x0f70);
+          else
+            __builtin_amdgcn_s_waitcnt((n1c & 15) | ((n1c >> 4) << 14) | 0x0f70);
+        } else {
+          vm_wait_all();
+        }
         __syncthreads();
-        buf ^= 1;
+        buf = RING == 3 ? (buf == 2 ? 0 : buf + 1) : buf ^ 1;
       }
     }
     pair = nxt;
@@ -1481,7 +1525,7 @@ dq_done:
   if ((stages & 8) && BIAS && a.dbias && a.seqlen_q > 0 && a.seqlen_k > 0) {
     const int bb = a.bias_stride[0] != 0 ? a.batch : 1, hb = a.bias_stride[1] != 0 ? a.heads_q : 1;
     const int nkc = ((a.seqlen_k + 63) / 64 + kDbiasChunk - 1) / kDbiasChunk;
-    dim3 grid(dbias_squares((a.seqlen_q + 127) / 128, nkc) * kDbiasSq * kDbiasSq, bb * hb);
+    dim3 grid(dbias_blocks((a.seqlen_q + 127) / 128, nkc), bb * hb);
     hipLaunchKernelGGL((dbias_kernel<BF16, DT, CAUSAL, DROPOUT, ALIGNED>), grid, dim3(256), 0, st, a);
   }
   if ((stages & 2) && a.seqlen_k > 0) {
