@@ -1170,7 +1170,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 // dQ GEMM; the next K/V tile and the next pair's Q/dO rows stream into LDS while the current
 // pair computes.
 // delta comes from the dQ (or delta) kernel that ran before (-rowsum(O dO), negated).
-constexpr int kDbiasChunk = 2;  // 64-key tiles per dbias workgroup
+// 64-key tiles per dbias workgroup.  One: the block's sums and bias (32 + 32 fp32 per lane) leave
+// the arch VGPRs room to read the K/V fragments ahead of the MFMAs; with two (64 + 64) the
+// compiler read each fragment just before its MFMA and waited out the LDS latency every time.
+constexpr int kDbiasChunk = 1;
 
 // XCD-aware block order: workgroup g runs on XCD g % 8 as that XCD's (g / 8)-th; the blocks go
 // out in 8 x 8 squares of (row block, key chunk), so the workgroups an XCD runs together share
@@ -1199,7 +1202,7 @@ FA2_DEV void dbias_block(int g, int nmb, int nkc, int& mb, int& kc) {
 }
 
 template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
-__global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr int NT = 256, BM = 128, BN = 64, C = kDbiasChunk;
   constexpr int KS = DT / 16;
@@ -1213,9 +1216,9 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
   // K/V tiles: a ring of 3 (D <= 128; staged two steps ahead) or 2 (D = 256, one step ahead)
   constexpr int RING = QLDS ? 3 : 2;
   // the deep pipeline counts its loads: fixed VMEM instructions per step (LDS-DMA pieces per
-  // K/V tile and per Q/dO block, plus the two -LSE / -delta loads), then "all but this step's"
-  constexpr int KV_VM = 2 * BufStager<DT, BN, NT>::kIters, QO_VM = 2 * BufStager<DT, BM, NT>::kIters + 2;
-  constexpr bool DEEP = QLDS && ALIGNED && !DROPOUT && C == 2;
+  // K/V tile and per Q/dO block; the two -LSE / -delta loads land before those go out)
+  constexpr int KV_VM = 2 * BufStager<DT, BN, NT>::kIters, QO_VM = 2 * BufStager<DT, BM, NT>::kIters;
+  constexpr bool DEEP = QLDS && ALIGNED && !DROPOUT;
   __shared__ __attribute__((aligned(16))) char smem[2 * RING * TILE + 2 * QTILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1363,7 +1366,10 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
     }
     const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride;
     // (unconditional loads, so that the step's VMEM count is fixed; row 0 exists: Lq > 0)
-    const float lse_v = p.lse[srow + (qvalid ? qi : 0)], del_v = p.delta[srow + (qvalid ? qi : 0)];
+    float lse_v = p.lse[srow + (qvalid ? qi : 0)], del_v = p.delta[srow + (qvalid ? qi : 0)];
+    // landed before this step's LDS-DMA goes out: the compiler's own wait for them counts no
+    // LDS-DMA, so waited at their use it would be a vmcnt(0) that drains this step's prefetches
+    asm volatile("" : "+v"(lse_v), "+v"(del_v));
     const float nlse = qvalid ? -lse_v : 0.f;
     const float ndel = qvalid ? del_v : 0.f;  // the workspace holds -delta
     if constexpr (QLDS) {
@@ -1398,6 +1404,20 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
         const char* K = kt(buf);
         const char* V = vt(buf);
         const int rel = lim_lane - n0 - 4 * hh;
+        // the tile's K / V fragments of both key halves, read ahead of the MFMAs (read next to
+        // each MFMA, every one of them waited out the LDS latency)
+        // (D = 256: read next to the MFMAs, the register file would not hold them)
+        u32x4 kf[2][QLDS ? KS : 1], vf[2][QLDS ? KS : 1];
+        if (QLDS && it < r.tend) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              kf[t][QLDS ? ks : 0] = lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh);
+              vf[t][QLDS ? ks : 0] = lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh);
+            }
+          __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink each read to its MFMA)
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           if (it >= r.tend) break;  // a ring step over a tile this pair does not see
@@ -1409,8 +1429,13 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
           f32x16 s = zero16(), dp = zero16();
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
-            dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
+            if constexpr (QLDS) {
+              s = E::mfma(kf[t][ks], qf[ks], s);
+              dp = E::mfma(vf[t][ks], of[ks], dp);
+            } else {
+              s = E::mfma(lds_row_frag<DT, BN>(K, 32 * t, r32, ks, hh), qf[ks], s);
+              dp = E::mfma(lds_row_frag<DT, BN>(V, 32 * t, r32, ks, hh), of[ks], dp);
+            }
           }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
@@ -1427,11 +1452,12 @@ __global__ void __launch_bounds__(256, DT <= 64 ? 2 : 1) dbias_kernel(const fa2_
           }
         }
         if constexpr (DEEP) {
-          // everything but this step's loads: the next step's tile (and, at a pair's end, the
-          // next pair's Q / dO) has landed; s_waitcnt vmcnt(n): bits 3:0 and 15:14 of the count
+          // all but the loads this step issued after what the next step needs: the next step's
+          // tile, and at a pair's last step the next pair's Q / dO (issued at its first step,
+          // before that step's K/V); s_waitcnt vmcnt(n): bits 3:0 and 15:14 of the count
           static_assert(KV_VM + QO_VM < 64, "vmcnt range");
           constexpr int n0c = KV_VM + QO_VM, n1c = KV_VM;
-          if (c == 0)
+          if (c < C - 1)
             __builtin_amdgcn_s_waitcnt((n0c & 15) | ((n0c >> 4) << 14) | 0x0f70);
           else
             __builtin_amdgcn_s_waitcnt((n1c & 15) | ((n1c >> 4) << 14) | 0x0f70);

@@ -182,3 +182,11 @@ def test_accumulators_untouched_until_read(tmp_path, kind):
                     i = j
                 i += 1
     assert checked > 0, f"no {kind} main statement found"
+
+
+def test_bias_gradient_kernels_have_no_scratch(kernels):
+    """dbias_kernel (round-4 restructure: the block's sums in registers over the broadcast group)
+    in every instantiation -- dtypes, head-dim tiles, causal, dropout, alignment -- spills nothing."""
+    found = {k: v for k, v in kernels.items() if "dbias_kernel" in k}
+    assert len(found) == 64, sorted(found)
+    assert not {k: v[0] for k, v in found.items() if v[0]}, "scratch bytes per lane"
