@@ -498,10 +498,10 @@ def main():
     workload_ok = (b, h, hkv, s, d, causal, dtype, fwd_only, plain) == (8, 32, 32, 4096, 128, True, torch.bfloat16, False,
                                                                        True)
     dominant = max(times, key=lambda n: times[n])
-    # device symbols the workload dispatches to (the pipelined forward: aligned D, no bias, no dropout)
-    hp_fwd = plain and d == 128 and os.environ.get("FA2_FWD_HP", "1") != "0"
-    hp_dkdv = plain and d == 128 and os.environ.get("FA2_DKDV_HP", "1") != "0"
-    hp_dq = plain and d == 128 and os.environ.get("FA2_DQ_HP", "1") != "0"
+    # device symbols the workload dispatches to (the hand-placed kernels: D = 128, aligned, no bias,
+    # no dropout -- the dropout dQ also, with the saved keep words)
+    hp_fwd = hp_dkdv = plain and d == 128
+    hp_dq = d == 128 and d % 8 == 0 and bias is None
     symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if plain else "fwd_kernel"),
               "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel",
               "dq_kernel": "dq_hp_kernel" if hp_dq else "dq_kernel", "dbias_kernel": "dbias_kernel"}

@@ -103,11 +103,13 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 6  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 7  # FA2_ABI_VERSION in include/fa2_amd.h
 
 EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes", "fa2_dropout_mask_bytes",
-                    "fa2_cu_seqlens_from_mask",
+                    "fa2_cu_seqlens_from_mask", "fa2_set_path_policy",
                     "fa2_last_error", "fa2_version")
+# fa2_path bits (fa2_set_path_policy)
+PATH_FWD_HP, PATH_DQ_HP, PATH_DKDV_HP = 1, 2, 4
 
 _lock = threading.Lock()
 _lib = None
@@ -142,6 +144,8 @@ def load() -> ctypes.CDLL:
         lib.fa2_last_error.restype = ctypes.c_char_p
         lib.fa2_dropout_mask_bytes.argtypes = [ctypes.c_int32] * 4
         lib.fa2_dropout_mask_bytes.restype = ctypes.c_int64
+        lib.fa2_set_path_policy.argtypes = [ctypes.c_uint32, ctypes.c_int32]
+        lib.fa2_set_path_policy.restype = ctypes.c_int
         lib.fa2_version.argtypes = []
         lib.fa2_version.restype = ctypes.c_int
         version = lib.fa2_version()
@@ -161,3 +165,9 @@ def check(rc: int) -> None:
     if rc == FA2_E_INVALID:
         raise ValueError(msg)
     raise RuntimeError(f"fa2_triton_amd: {msg} (status {rc})")
+
+
+def set_path_policy(disable: int = 0, grid_cap: int = 0) -> None:
+    """fa2_set_path_policy: turn the hand-placed paths named by `disable` (PATH_* bits) off and cap
+    the persistent kernels' grid (0: one workgroup per CU).  (0, 0) restores the defaults."""
+    check(load().fa2_set_path_policy(disable, grid_cap))

@@ -68,11 +68,25 @@ hipError_t dispatch_dt(int dt, F4 f32, F8 f64, F12 f128, F16 f256) {
 
 }  // namespace
 
+namespace fa2 {
+volatile uint32_t g_path_disable = 0;
+volatile int32_t g_grid_cap = 0;
+}  // namespace fa2
+
 extern "C" {
 
 int fa2_version(void) { return FA2_ABI_VERSION; }
 
 const char* fa2_last_error(void) { return g_err; }
+
+int fa2_set_path_policy(uint32_t disable, int32_t grid_cap) {
+  if (disable & ~(uint32_t)(FA2_PATH_FWD_HP | FA2_PATH_DQ_HP | FA2_PATH_DKDV_HP))
+    return fail(FA2_E_INVALID, "unknown path bits 0x%x", disable);
+  if (grid_cap < 0) return fail(FA2_E_INVALID, "grid_cap %d < 0", grid_cap);
+  fa2::g_path_disable = disable;
+  fa2::g_grid_cap = grid_cap;
+  return FA2_OK;
+}
 
 int fa2_fwd(const fa2_fwd_args* a, void* stream) {
   if (!a) return fail(FA2_E_INVALID, "null args");

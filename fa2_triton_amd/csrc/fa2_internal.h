@@ -6,6 +6,12 @@
 
 namespace fa2 {
 
+// fa2_set_path_policy (api.hip): bits of fa2_path disabled, persistent-grid cap (0: none)
+extern volatile uint32_t g_path_disable;
+extern volatile int32_t g_grid_cap;
+inline bool path_on(uint32_t bit) { return !(g_path_disable & bit); }
+inline int capped_grid(int ncu) { const int c = g_grid_cap; return c > 0 && c < ncu ? c : ncu; }
+
 // Forward, one translation unit per (dtype, head-dim tile); see fwd_inst.hip.
 template <bool BF16, int DT>
 hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st);

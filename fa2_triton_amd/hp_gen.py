@@ -26,6 +26,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GEN = os.path.join(HERE, "csrc", "gen")
+# development timing ablations (wrong outputs; never set for a shipped build): FA2_HPGEN_ABL=a,b
+ABL = set(filter(None, os.environ.get("FA2_HPGEN_ABL", "").split(",")))
 
 NINF = "0xff800000"
 
@@ -928,18 +930,26 @@ class FwdGen:
 #
 # Register map of the statement:
 #   v[0:31]     S[kb] accumulators, then P = exp2(acc scale log2 e - LSE2) in place
-#   v[32:63]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place
-#   v[64:79]    PP[kb][sp] packed P (B operand of dV^T += dO^T P), v[80:95] DSP[kb][sp] packed dS
-#   v[96:111]   row-fragment ring (Q then dO, A operands of S and dP), 4 slots
-#   v[112:131]  V fragment ring (B operands of dP), 5 slots
-#   v[132:147]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
-#   v[148:151]  mask bounds LO[kb], HI[kb] of a masked step
-#   v[152:167]  LSE2 of the 16 rows of this lane's registers (read per step from LDS)
+#   v[32:63]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place, then
+#               in place the packed dS DSP[kb][sp] (B operands of dK^T += Q^T dS)
+#   v[64:79]    PP[kb][sp] packed P (B operand of dV^T += dO^T P)
+#   v[80:95]    row-fragment ring (Q then dO, A operands of S and dP), 4 slots
+#   v[96:115]   V fragment ring (B operands of dP), 5 slots
+#   v[116:131]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
+#   v[132:135]  mask bounds LO[kb], HI[kb] of a masked step
+#   v[136:151]  LSE2 of the 16 rows of this lane's registers (read per step from LDS)
 #   a[0:127]    dV^T[kb][dt], a[128:255] dK^T[kb][dt]
 #   K fragments: compiler-placed "v" operands %[k0]..%[k15]
-# LDS (bytes from the workgroup's base): Q tile of buffer b at 16384 b, dO tile at 16384 b + 8192
-# (Tile<128, 32>), V rows of wave w at 32768 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of
-# buffer b at 98304 + 256 b (+128).
+# LDS (bytes from the workgroup's base): a ring of DK_NBUF = 3 step buffers (the step i + 2's
+# tiles are requested during step i): Q tile of buffer b at 16384 b, dO tile at 16384 b + 8192
+# (Tile<128, 32>), V rows of wave w at DK_V0 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of
+# buffer b at DK_ROWS + 256 b (+128).
+DK_NBUF = 3
+DK_V0 = 16384 * DK_NBUF
+DK_ROWS = DK_V0 + 65536
+DK_LDS = DK_ROWS + 256 * DK_NBUF
+DK_AHEAD = DK_NBUF - 1  # steps of lead of a step's DMA
+DK_VMEM = 4  # vector-memory ops of one step's DMA after its rows (the count each step end leaves)
 def DS(kb, i=None):
     return rng("v", 16 * kb, 16) if i is None else f"v{16 * kb + i}"
 
@@ -954,36 +964,39 @@ def DPP(kb, sp, j=None):
 
 
 def DDSP(kb, sp, j=None):
-    base = 80 + (kb * 2 + sp) * 4
+    """Packed dS of 16-row step sp, in place over dP[kb] (as QDSP): pack j of elements 8 sp ..
+    8 sp + 7 reads 2j, 2j + 1 and writes element j."""
+    base = 32 + 16 * kb + 8 * sp
     return rng("v", base, 4) if j is None else f"v{base + j}"
 
 
 def DRR(n):
-    return rng("v", 96 + 4 * (n % 4), 4)
+    return rng("v", 80 + 4 * (n % 4), 4)
 
 
 DVF_SLOTS = 5
 
 
 def DVF(n):
-    return rng("v", 112 + 4 * (n % DVF_SLOTS), 4)
+    return rng("v", 96 + 4 * (n % DVF_SLOTS), 4)
 
 
 def DTR(n, half=None):
-    base = 132 + 4 * (n % 4)
+    base = 116 + 4 * (n % 4)
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-DLO = ["v148", "v149"]
-DHI = ["v150", "v151"]
+DLO = ["v132", "v133"]
+DHI = ["v134", "v135"]
+DLSE0 = 136
 
 
 def DLSE(i):
     """LSE2 of the row of register i (rows (i & 3) + 8 (i >> 2) + 4 hh of the step's tile)."""
-    return f"v{152 + i}"
+    return f"v{DLSE0 + i}"
 
 
-DK_NVGPR = 168
+DK_NVGPR = 152
 
 
 def DDV(kb, dt):
@@ -1059,7 +1072,7 @@ class DkdvGen:
         """LSE2 (what 0) rows into the LSE registers, -delta (what 1) into dP[kb] (the dP
         chain's initial accumulator): register group g4."""
         imm = par * 256 + what * 128 + 32 * g4
-        d = rng("v", 152 + 4 * g4, 4) if what == 0 else rng("v", 32 + 16 * kb + 4 * g4, 4)
+        d = rng("v", DLSE0 + 4 * g4, 4) if what == 0 else rng("v", 32 + 16 * kb + 4 * g4, 4)
         self.e.ds_read(f"ds_read_b128 {d}, %[lb] offset:{imm}", d)
 
     def descriptors(self):
@@ -1067,7 +1080,7 @@ class DkdvGen:
         e = self.e
         t2 = "s94"  # (D_EX, free until the rows' DMA)
         e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
-        e.salu(f"s_cmp_gt_u32 {D_LEFT}, 0")
+        e.salu(f"s_cmp_gt_i32 {D_LEFT}, 0")
         e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
         e.salu(f"s_cselect_b32 {t2}, 128, 0")
         for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
@@ -1106,9 +1119,10 @@ class DkdvGen:
         e.label(f".Lhp%=_{tag}_adv")
 
     def dma_items(self, par, tag):
-        """The step's DMA pieces (Q, dO of the next step into buffer 1 - par; wave 0 also its
-        LSE2 / delta rows) as (cost, emit) items; m0 is set one item ahead."""
-        nb = 1 - par
+        """The step's DMA (wave 0: the LSE2 / delta rows first; then the Q, dO pieces) of the
+        step DK_AHEAD later into buffer (par + DK_AHEAD) mod DK_NBUF, as (cost, emit) items; m0
+        is set one item ahead.  Every wave's last DK_VMEM vector-memory ops are its pieces."""
+        nb = (par + DK_AHEAD) % DK_NBUF
         pieces = [("q", 0), ("q", 1), ("o", 0), ("o", 1)]
 
         def m0_of(w_, it):
@@ -1137,8 +1151,7 @@ class DkdvGen:
             e.dma(f"buffer_load_dwordx4 %[lsoff], {D_DD}, 0 offen lds")
             e.salu(f"s_mov_b64 exec, {D_EX}")
             e.label(f".Lhp%=_{tag}_nl")
-        out.append((16, rows))
-        return out
+        return [(16, rows)] + out
 
     def mask_elem(self, kb, i):
         """P = LO[kb] <= o < HI[kb] ? P : 0 for the register i of key block kb (o = row offset)."""
@@ -1213,7 +1226,10 @@ class DkdvGen:
                 for h in range(2):
                     g.add("tr", 4, rel, mf - 3, lambda n=n, h=h: self.tr_read(par, n, h))
             for n, (c, f) in enumerate(dma):
-                g.add("dma", c, 2, 40 + n, f)
+                if "dk_nodma" not in ABL:
+                    g.add("dma", c, 2, 40 + n, f)
+            if "dk_novalu" in ABL:
+                g.items = [it for it in g.items if not it["stream"].startswith(("exp", "ds"))]
 
             def mfma(i):
                 if i < 16:  # S[kb] += Q(ks) K[kb](ks)
@@ -1233,12 +1249,15 @@ class DkdvGen:
 
             g.run(mfma, pre_budget=48)
         self.advance_cursors(tag)
-        e.salu(f"s_sub_u32 {D_LEFT}, {D_LEFT}, 1")
+        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
         e.salu(f"s_sub_u32 {D_CM}, {D_CM}, 32")
-        e.salu(f"s_xor_b32 {D_PAR}, {D_PAR}, 1")
+        e.salu(f"s_mov_b32 {D_PAR}, {(par + 1) % DK_NBUF}")
         e.drain_lds()
-        e.raw("s_waitcnt vmcnt(0)")
-        e.raw("s_barrier")
+        if "dk_novm" not in ABL:
+            # the next step's tiles (requested one step ago) have landed; this step's stay in flight
+            e.raw(f"s_waitcnt vmcnt({DK_VMEM})")
+        if "dk_nobar" not in ABL:
+            e.raw("s_barrier")
         e.reset()
 
     def cvt(self, d, a, b):
@@ -1260,11 +1279,19 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
         self.advance_cursors("init")
+        # step 0's tiles were requested before the statement (and waited for by the compiler's
+        # wait for the K fragments); step 1's into buffer 1 here, then the cursors go to step 2.
+        # D_LEFT = steps after the one requested next: at step i, total - 2 - i (signed)
         e.salu(f"s_mov_b32 {D_LEFT}, %[total]")
-        e.salu(f"s_sub_u32 {D_LEFT}, {D_LEFT}, 1")
+        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
+        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.descriptors()
+        for _, f in self.dma_items((1 - DK_AHEAD) % DK_NBUF, "pro"):
+            f()
+        self.advance_cursors("init2")
+        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
         e.salu(f"s_mov_b32 {D_G}, 0")
         e.salu(f"s_mov_b32 {D_PAR}, 0")
-        e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
         e.reset()
         e.raw("s_cmp_eq_u32 %[total], 0")
@@ -1282,20 +1309,24 @@ class DkdvGen:
         e.raw("s_cbranch_scc1 .Lhp%=_clsA")
         e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c012]")
         e.raw("s_cbranch_scc1 .Lhp%=_clsB")
-        e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
-        e.raw("s_cbranch_scc1 .Lhp%=_D0")
-        e.raw("s_branch .Lhp%=_D1")
-        e.label(".Lhp%=_clsA")
-        e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
-        e.raw("s_cbranch_scc0 .Lhp%=_A1")
-        for cls, par in (("A", 0), ("A", 1), ("B", 0), ("B", 1), ("D", 0), ("D", 1)):
-            if (cls, par) == ("B", 0):
-                e.label(".Lhp%=_clsB")
-                e.raw(f"s_cmp_eq_u32 {D_PAR}, 0")
-                e.raw("s_cbranch_scc0 .Lhp%=_B1")
-            e.label(f".Lhp%=_{cls}{par}")
-            self.step(par, cls, f"{cls.lower()}{par}")
-            e.raw("s_branch .Lhp%=_next")
+        e.label(".Lhp%=_clsD")
+
+        def dispatch(cls):
+            # buffer parity D_PAR in 0 .. DK_NBUF - 1 -> the step body of that parity
+            for par in range(DK_NBUF - 1):
+                e.raw(f"s_cmp_eq_u32 {D_PAR}, {par}")
+                e.raw(f"s_cbranch_scc1 .Lhp%=_{cls}{par}")
+            e.raw(f"s_branch .Lhp%=_{cls}{DK_NBUF - 1}")
+
+        dispatch("D")
+        for cls in ("A", "B", "D"):
+            if cls != "D":
+                e.label(f".Lhp%=_cls{cls}")
+                dispatch(cls)
+            for par in range(DK_NBUF):
+                e.label(f".Lhp%=_{cls}{par}")
+                self.step(par, cls, f"{cls.lower()}{par}")
+                e.raw("s_branch .Lhp%=_next")
         e.label(".Lhp%=_next")
         e.salu(f"s_add_u32 {D_IDX}, {D_IDX}, 1")
         e.raw(f"s_cmp_lt_u32 {D_IDX}, %[nmt]")
@@ -1304,7 +1335,10 @@ class DkdvGen:
         e.raw(f"s_cmp_lt_u32 {D_G}, %[ng]")
         e.raw("s_cbranch_scc1 .Lhp%=_head")
         e.label(".Lhp%=_end")
+        # every wave's (range-0) requests of the last steps have landed before any wave stages
+        # its epilogue in the step buffers
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.raw("s_barrier")
         e.salu(f"s_mov_b32 m0, {D_M0}")
         e.raw("s_nop 15")
         e.raw("s_nop 15")
@@ -1316,7 +1350,7 @@ def gen_dkdv_function(bf16, causal):
     lines = g.build()
     name = f"dkdv_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
     clob = [f'"v{i}"' for i in range(DK_NVGPR)] + [f'"a{i}"' for i in range(256)] + \
-           [f'"s{i}"' for i in D_SGPR_CLOBBER] + ['"vcc"', '"scc"', '"memory"']
+           [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
     sops = ["ng", "nmt", "total", "c0", "c01", "c012", "mlast", "lq", "qrb", "orb", "qtile", "otile", "qwrap",
             "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
@@ -1361,10 +1395,10 @@ def gen_read_dkdv():
 # dQ: dq_hp_kernel (csrc/dq_hp_kernel.h)
 #
 # Register map of the statement:
-#   v[0:63]     S^T[rb][h] (scores of key half h; then P), v[64:127] dP^T[rb][h] (then dS)
-#   v[128:159]  DSP[rb][kk] packed dS^T (B operand of dQ^T += K^T dS^T)
-#   v[160:175]  K row-fragment ring, v[176:191] V row-fragment ring, v[192:207] K^T ring
-#   v[208:209]  mask limits of a masked tile
+#   v[0:63]     S^T[rb][h] (scores of key half h; then P), v[64:127] dP^T[rb][h] (then dS, then
+#               in place the packed dS^T DSP[rb][kk]: the B operands of dQ^T += K^T dS^T)
+#   v[128:143]  K row-fragment ring, v[144:159] V row-fragment ring, v[160:175] K^T ring
+#   v[176:177]  mask limits of a masked tile
 #   a[0:127]    dQ^T[rb][dt]; a[128:255] the Q and dO fragments ("a" operands)
 def QS(rb, h, i=None):
     base = (rb * 2 + h) * 16
@@ -1377,40 +1411,43 @@ def QDP(rb, h, i=None):
 
 
 def QDSP(rb, kk, j=None):
-    base = 128 + (rb * 4 + kk) * 4
+    """Packed dS^T of 16-key step kk, in place over dP^T[rb][kk >> 1]: pack j of the 8-element
+    group 8 (kk & 1) .. + 7 reads elements 2j, 2j + 1 and writes element j (consumed by pack j // 2,
+    issued before it in the same stream), so the four packs land in consecutive registers."""
+    base = 64 + (rb * 2 + (kk >> 1)) * 16 + 8 * (kk & 1)
     return rng("v", base, 4) if j is None else f"v{base + j}"
 
 
 def QKR(n):
-    return rng("v", 160 + 4 * (n % 4), 4)
+    return rng("v", 128 + 4 * (n % 4), 4)
 
 
 def QVR(n):
-    return rng("v", 176 + 4 * (n % 4), 4)
+    return rng("v", 144 + 4 * (n % 4), 4)
 
 
 def QTR(n, half=None):
-    base = 192 + 4 * (n % 4)
+    base = 160 + 4 * (n % 4)
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-QREL = ["v208", "v209"]
-DQ_NVGPR = 210
+QREL = ["v176", "v177"]
+DQ_NVGPR = 178
 # dropout (the forward's saved keep words, one 32-key word per row): the words of the current and
 # the next tile, per (rb, key half h); per-stream temporaries; the lane's word offsets (cursor)
 def QMW(st, rb, h):
-    return f"v{210 + 4 * st + 2 * rb + h}"
+    return f"v{DQ_NVGPR + 4 * st + 2 * rb + h}"
 
 
 def QMT(h, rb):
     """dS temporaries: the K ring's slot 0, free once the S chains are issued (the dS phase
     starts 18 MFMAs later)."""
-    return f"v{160 + 2 * h + rb}"
+    return f"v{128 + 2 * h + rb}"
 
 
-QMO = "v218"       # lane byte offset of row block 0's tile-0 words (row block 1: + %[mrs])
-DQ_NVGPR_DROP = 219
-Q_MD = "s[92:95]"  # keep-word descriptor
+QMO = f"v{DQ_NVGPR + 8}"  # lane byte offset of row block 0's tile-0 words (row block 1: + %[mrs])
+DQ_NVGPR_DROP = DQ_NVGPR + 9
+Q_MD = "%[mdesc]"  # keep-word descriptor (a 4-SGPR operand)
 Q_MOFF = ["s96", "s97"]  # byte offsets of the requested tile's words, row block 0 / 1
 
 
@@ -1591,7 +1628,8 @@ class DqGen:
         e.salu(f"s_add_i32 {Q_SN0}, {Q_SN0}, 64")
         e.salu(f"s_xor_b32 {Q_PAR}, {Q_PAR}, 1")
         e.drain_lds()
-        e.raw("s_waitcnt vmcnt(0)")
+        if "dq_novm" not in ABL:
+            e.raw("s_waitcnt vmcnt(0)")
         e.raw("s_barrier")
         e.reset()
 
@@ -1640,10 +1678,6 @@ class DqGen:
         if self.dropout:
             # keep words: tile 0's in %[mw*] (from the previous unit or the caller) -> both sets;
             # period i requests tile i + 1's
-            e.salu("s_mov_b32 s92, %[mklo]")
-            e.salu("s_and_b32 s93, %[mkhi], 0xffff")
-            e.salu("s_mov_b32 s94, %[mkbytes]")
-            e.salu("s_mov_b32 s95, 0x20000")
             e.salu(f"s_mov_b32 {Q_MOFF[0]}, 256")
             e.salu(f"s_add_u32 {Q_MOFF[1]}, %[mrs], 256")
             e.valu(f"v_mov_b32 {QMO}, %[mo0]", QMO)
@@ -1722,7 +1756,11 @@ class DqGen:
                 if st == 0:
                     e.raw("s_branch .Lhp%=_mwd")
             e.label(".Lhp%=_mwd")
-        self.next_unit_loads()
+        else:
+            # the next unit's Q / dO straight into the operand registers, left in flight across the
+            # epilogue (the dropout variant loads them in its own statement after the epilogue:
+            # gen_dq_load_next, nothing in flight between statements)
+            self.next_unit_loads()
         e.drain_lds()
         e.salu(f"s_mov_b32 m0, {SM0}")
         e.raw("s_nop 15")
@@ -1748,21 +1786,22 @@ def gen_dq_function(bf16, causal, dropout=False):
     lines = g.build()
     name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_drop' if dropout else ''}"
     nv = DQ_NVGPR_DROP if dropout else DQ_NVGPR
-    sg = SGPR_CLOBBER + (list(range(92, 98)) if dropout else [])
     clob = [f'"v{i}"' for i in range(nv)] + [f'"a{i}"' for i in range(128)] + \
-           [f'"s{i}"' for i in sg] + ['"vcc"', '"scc"', '"memory"']
+           [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
     qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
     oops = ", ".join(f'[o{i}] "+a"(o[{i}])' for i in range(16))
     mops = (",\n        " + ", ".join(f'[mw{i}] "+v"(mw[{i}])' for i in range(4))) if dropout else ""
-    vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1",
-            "nqo0", "noo0"] + (["mo0", "nmo0", "msh"] if dropout else [])
+    nxt_v = [] if dropout else ["nqo0", "noo0"]
+    nxt_s = [] if dropout else ["nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes", "nqrs", "nors"]
+    vops = ["kb0", "kb1", "ta", "tb", "off0", "off1", "off2", "off3", "rel0", "rel1", "lse0", "lse1", "del0", "del1"] + \
+        nxt_v + (["mo0", "nmo0", "msh"] if dropout else [])
     sops = ["na", "last", "ntiles", "tileb", "kbytes", "mlds", "klo", "khi", "vlo", "vhi", "sc",
-            "boff", "nklo", "nkhi", "nvlo", "nvhi", "nkbytes", "nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes",
-            "nqrs", "nors"] + (["mklo", "mkhi", "mkbytes", "mrs", "dsc"] if dropout else [])
+            "boff", "nklo", "nkhi", "nvlo", "nvhi", "nkbytes"] + nxt_s + (["mdesc", "mrs", "dsc"] if dropout else [])
     marg = ", uint32_t (&mw)[4]" if dropout else ""
+    inout = ("this unit's Q and dO fragments in (the next unit's: gen_dq_load_next)" if dropout else
+             "this unit's Q and dO fragments in, the NEXT unit's out -- still in flight (wait before\n// reading them)")
     src = f"""// hand-placed dQ unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}{', dropout' if dropout else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
-// q / o: this unit's Q and dO fragments in, the NEXT unit's out -- still in flight (wait before
-// reading them){'; mw: the keep words of tile 0, in and (next unit) out' if dropout else ''}
+// q / o: {inout}{'; mw: the keep words of tile 0, in and (next unit) out' if dropout else ''}
 FA2_DEV void {name}(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a{marg}) {{
   asm volatile(
 {_asm_body(lines)}
@@ -1780,15 +1819,52 @@ def _asm_body(lines):
     return "\n".join(f'      "{l}\\n"' for l in lines)
 
 
+def _sgprs_used(lines):
+    """The fixed SGPRs a statement names (its clobbers: no more than it uses, so the compiler
+    keeps the rest for the values live across it)."""
+    used = set()
+    for l in lines:
+        for m in re.finditer(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b", l):
+            if m.group(3):
+                used.add(int(m.group(3)))
+            else:
+                used.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return sorted(used)
+
+
+def gen_dq_load_next():
+    """The dropout dQ's next-unit Q / dO fragments: loads and their wait in ONE statement (outputs
+    early-clobber), so no load is in flight while compiler code runs (the compiler
+    moved in-flight "+a" operands of the spilling dropout variant and read them early)."""
+    g = DqGen(True, False, False)
+    g.next_unit_loads()
+    # s_nop 12: marker of tests/test_code_objects.py (end of the in-flight window: none here)
+    lines = ["s_nop 12"] + g.e.out + ["s_waitcnt vmcnt(0)"]
+    qops = ", ".join(f'[q{i}] "=&a"(q[{i}])' for i in range(16))
+    oops = ", ".join(f'[o{i}] "=&a"(o[{i}])' for i in range(16))
+    ins = ", ".join([f'[{n}] "v"(a.{n})' for n in ("nqo0", "noo0")] +
+                    [f'[{n}] "s"(a.{n})' for n in ("nqlo", "nqhi", "nqbytes", "nolo", "nohi", "nobytes", "nqrs", "nors")])
+    clob = ", ".join([f'"s{i}"' for i in _sgprs_used(lines)] + ['"memory"'])
+    return f"""// the next unit's Q / dO fragments (dropout dQ), loaded and waited for in one statement
+FA2_DEV void dq_hp_load_next(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a) {{
+  asm volatile(
+{_asm_body(lines)}
+      : {qops},
+        {oops}
+      : {ins}
+      : {clob});
+}}
+"""
+
+
 def gen_fwd_function(bf16, causal, exact=True):
     out = []
     for stamp in (False, True):
         g = FwdGen(bf16, causal, exact, stamp)
         lines = g.build()
         name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
-        sg = SGPR_CLOBBER + (list(range(92, 102)) if stamp else [])
         clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
-               [f'"s{i}"' for i in sg] + ['"vcc"', '"scc"', '"memory"']
+               [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
         qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
         stops = ", " + ", ".join(f'[st{i}] "=&s"(st[{i}])' for i in range(4)) if stamp else ""
         starg = ", uint32_t (&st)[4]" if stamp else ""
@@ -1858,6 +1934,7 @@ def write_headers():
         for causal in (True, False):
             for dropout in (False, True):
                 out.append(gen_dq_function(bf16, causal, dropout))
+    out.append(gen_dq_load_next())
     out.append(gen_read_o().replace("fwd_hp_read_o", "dq_hp_read").replace("O^T accumulators", "dQ^T accumulators"))
     out.append("}  // namespace fa2\n")
     paths.append(_write(os.path.join(GEN, "dq_hp_body.h"), "\n".join(out)))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 6
+#define FA2_ABI_VERSION 7
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -164,6 +164,17 @@ int64_t fa2_dropout_mask_bytes(int32_t batch, int32_t heads_q, int32_t seqlen_q,
  * .item() syncs of the reference callers (src/forward/caller.py:48-50, src/utils.py:8-17). */
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch,
                              int32_t seqlen, int32_t* cu_seqlens, void* stream);
+
+/* Kernel-path policy (ABI 7), process-wide, read at every launch; for tests and A/B timing.
+ * Bits of `disable` turn a specialised path off so that the general kernels of the same launch
+ * run instead (same math; the tests compare the two): FA2_PATH_FWD_HP the hand-placed D = 128
+ * forward, FA2_PATH_DQ_HP / FA2_PATH_DKDV_HP the hand-placed D = 128 dQ / dK-dV.
+ * grid_cap > 0 caps the grid of the persistent (one workgroup per CU) kernels, so that small
+ * problems run several work units per workgroup.  Default (0, 0): every path on, one workgroup
+ * per CU.  Not synchronised with launches in flight on other threads.  The environment is
+ * never read. */
+enum fa2_path { FA2_PATH_FWD_HP = 1, FA2_PATH_DQ_HP = 2, FA2_PATH_DKDV_HP = 4 };
+int fa2_set_path_policy(uint32_t disable, int32_t grid_cap);
 
 const char* fa2_last_error(void);
 int fa2_version(void);

@@ -1,6 +1,6 @@
 """GPU dev check of the hand-placed forward (fwd_hp_kernel) against fwd_pipe_kernel and the oracle.
 
-For each shape: O and LSE2 from FA2_FWD_HP=1 and =0 in one process, max |diff| between them, and
+For each shape: O and LSE2 with the hand-placed forward on and off (fa2_set_path_policy) in one process, max |diff| between them, and
 each one's max |O - O_fp32 oracle|.  usage: python tests/hp_check.py
 """
 import os
@@ -9,6 +9,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fa2_triton_amd import _lib as L  # noqa: E402
 from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
 from oracle.reference import attention_reference, lse2_reference  # noqa: E402
 
@@ -33,10 +34,11 @@ def run(case):
     v = torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5
     res = {}
     for hp in ("1", "0"):
-        os.environ["FA2_FWD_HP"] = hp
+        L.set_path_policy(0 if hp == "1" else L.PATH_FWD_HP, 0)
         o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
         torch.cuda.synchronize()
         res[hp] = (o.float(), lse[:, :, :sq].float())
+    L.set_path_policy(0, 0)
     ref = attention_reference(q, k, v, causal=causal).float()
     pt = attention_reference(q, k, v, causal=causal, upcast=False, reorder_ops=True).float()
     lref = lse2_reference(q, k, causal=causal)
@@ -78,18 +80,15 @@ def run_bwd(case):
     k = (torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5).requires_grad_()
     v = (torch.randn(b, sk, hkv, 128, device="cuda", dtype=dt) * 0.5).requires_grad_()
     do = torch.randn(b, sq, hq, 128, device="cuda", dtype=dt)
-    os.environ["FA2_FWD_HP"] = "0"
+    L.set_path_policy(L.PATH_FWD_HP, 0)
     o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
     res = {}
     for hp in ("1", "0"):
-        os.environ["FA2_DKDV_HP"] = hp
-        os.environ["FA2_DQ_HP"] = hp
+        L.set_path_policy(L.PATH_FWD_HP | (0 if hp == "1" else L.PATH_DQ_HP | L.PATH_DKDV_HP), 0)
         g = _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None)
         torch.cuda.synchronize()
         res[hp] = [x.float() for x in g[:3]]
-    os.environ.pop("FA2_DKDV_HP")
-    os.environ.pop("FA2_DQ_HP")
-    os.environ.pop("FA2_FWD_HP")
+    L.set_path_policy(0, 0)
     ref = attention_reference(q, k, v, causal=causal)
     gref = torch.autograd.grad(ref, (q, k, v), do.float())
     pt = attention_reference(q, k, v, causal=causal, upcast=False, reorder_ops=True)

@@ -119,9 +119,9 @@ def test_every_kernel_fits_the_cu(kernels):
 
 # the hand-placed one-wave-per-SIMD kernels (hp_gen.py): whole register file, zero scratch
 HP = {
-    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_fwd_args",
+    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb1EEEv12fa2_fwd_args",
     "dkdv_hp": r"_ZN3fa214dkdv_hp_kernelILb[01]ELb[01]EEEv12fa2_bwd_argsi",
-    "dq_hp": r"_ZN3fa212dq_hp_kernelILb[01]ELb[01]ELb0EEEv12fa2_bwd_args",
+    "dq_hp": r"_ZN3fa212dq_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_bwd_args",
 }
 
 
@@ -129,7 +129,9 @@ HP = {
 def test_hand_placed_kernels_have_no_scratch(kernels, kind):
     pat = re.compile(HP[kind] + "$")
     found = {k: v for k, v in kernels.items() if pat.match(k)}
-    assert len(found) == (8 if kind == "fwd_hp" else 4), (kind, sorted(found))  # dtypes x causal (x exact)
+    # dtypes x causal (x dropout for dQ; the pre-scaled-Q forward exists only in development
+    # builds, FA2_HP_DEV)
+    assert len(found) == (8 if kind == "dq_hp" else 4), (kind, sorted(found))
     for k, (scratch, vgprs, lds) in found.items():
         assert scratch == 0, (k, scratch)
         assert vgprs <= 512 and lds <= 160 * 1024, (k, vgprs, lds)  # one workgroup of 4 waves per CU
@@ -190,3 +192,61 @@ def test_bias_gradient_kernels_have_no_scratch(kernels):
     found = {k: v for k, v in kernels.items() if "dbias_kernel" in k}
     assert len(found) == 64, sorted(found)
     assert not {k: v[0] for k, v in found.items() if v[0]}, "scratch bytes per lane"
+
+
+# The next unit's Q (forward) and Q / dO (dQ) fragments are loaded by the main statement's tail
+# straight into its "+a" operand registers and stay in flight across the compiler's epilogue
+# code: nothing may read, copy or overwrite those AGPRs before the wait (the
+# spilling dropout dQ moved them early and computed with garbage).  Windows checked on the ISA:
+# forward -- from the statement's closing `s_nop 15` pair to the function end, and from the loop
+# head marker (`s_nop 13`) to the next statement's opening `s_nop 7` pair; dQ -- from the closing
+# pair to the wait statement (`s_nop 14`).  The dropout dQ loads its next unit in a statement of
+# its own (loads and wait together, opening with `s_nop 12`), so nothing is in flight there.
+OPERANDS = {"fwd_hp": (128, 192), "dq_hp": (128, 256)}
+
+
+def _agpr_refs(line):
+    out = set()
+    for m in re.finditer(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b", line):
+        if m.group(3):
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+@pytest.mark.parametrize("kind", sorted(OPERANDS))
+def test_in_flight_operands_untouched(tmp_path, kind):
+    if not os.path.exists(_lib.LIB_PATH) or not os.path.exists(OBJDUMP):
+        pytest.skip("library or llvm-objdump missing")
+    lo, hi = OPERANDS[kind]
+    sym = {"fwd_hp": "fwd_hp_kernel", "dq_hp": "dq_hp_kernel"}[kind]
+    checked = 0
+    for n, co in enumerate(_code_objects(_lib.LIB_PATH)):
+        if sym.encode() not in co:
+            continue
+        text = _disassemble(co, tmp_path, n)
+        for func in re.split(r"\n(?=[0-9a-f]+ <)", text):
+            if sym not in func.split("\n", 1)[0]:
+                continue
+            lines = [ln.split("//")[0].strip() for ln in func.split("\n")[1:]]
+            lines = [ln for ln in lines if ln]
+            pairs = lambda op: [i for i in range(len(lines) - 1) if lines[i].startswith(op) and lines[i + 1].startswith(op)]
+            ends, starts = pairs("s_nop 15"), pairs("s_nop 7")
+            assert len(ends) == 1 and len(starts) == 1, (kind, len(ends), len(starts))
+            windows = []
+            if kind == "fwd_hp":
+                head = [i for i, ln in enumerate(lines) if ln.startswith("s_nop 13")]
+                assert len(head) == 1, head
+                windows = [(ends[0] + 2, len(lines)), (head[0] + 1, starts[0])]
+            else:
+                wait = [i for i, ln in enumerate(lines) if ln.startswith(("s_nop 14", "s_nop 12"))]
+                assert 1 <= len(wait) <= 2, wait
+                windows = [(ends[0] + 2, wait[0])]
+            for a, b in windows:
+                assert a <= b, (kind, a, b)
+                for ln in lines[a:b]:
+                    bad = {r for r in _agpr_refs(ln) if lo <= r < hi}
+                    assert not bad, (kind, ln)
+            checked += 1
+    assert checked > 0, f"no {kind} kernel found"

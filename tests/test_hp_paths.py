@@ -1,0 +1,135 @@
+"""The hand-placed D = 128 kernels against the general kernels of the same launch, and their
+persistent multi-unit paths.
+
+* Backward: the hand-placed dQ and dK/dV (`dq_hp_kernel`, `dkdv_hp_kernel`) compute the same
+  fp32 sums in the same order as `dq_kernel` / `dkdv_kernel` (same math as the reference's loops,
+  /root/reference/src/backward/compute_dq.py:38-78, compute_dkdv.py:42-112), so dQ, dK, dV must be
+  BITWISE equal with the hand-placed paths on and off (fa2_set_path_policy, ABI 7).
+* Forward: `fwd_hp_kernel` and `fwd_pipe_kernel` order the softmax differently (defer-max
+  thresholds, tile phases): both within the reference's tolerance of the oracle, LSE2 within 1e-3.
+* Persistence: one workgroup per CU walks several work units when the grid is capped
+  (grid_cap = 2 or 3: every workgroup runs many units, so the next-unit prefetch, buffer parity
+  and the hand-off of Q / dO / keep words across units all run).  Results must be bitwise equal
+  to the uncapped launch -- with dropout too (the keep words of the next unit are loaded by the
+  previous unit's statement).
+"""
+import pytest
+import torch
+
+from tests.core import generate_attention_mask, generate_test_data
+
+BWD_CASES = [
+    # b, hq, hkv, sq, sk, causal, dtype
+    (1, 1, 1, 256, 256, False, torch.bfloat16),
+    (1, 1, 1, 256, 256, True, torch.bfloat16),
+    (2, 4, 2, 512, 512, True, torch.bfloat16),
+    (2, 4, 4, 1024, 1024, False, torch.float16),
+    (1, 2, 1, 300, 700, True, torch.bfloat16),
+    (1, 2, 2, 777, 333, True, torch.float16),
+    (1, 4, 1, 129, 257, False, torch.bfloat16),
+    (2, 8, 8, 2048, 2048, True, torch.bfloat16),
+]
+
+
+@pytest.fixture
+def policy():
+    from fa2_triton_amd import _lib as L
+
+    yield L
+    L.set_path_policy(0, 0)
+
+
+def _fwd_bwd(q, k, v, do, causal, mask=None, dropout_p=0.0, seed=None, policy=None, disable=0, cap=0):
+    from fa2_triton_amd import flash_attn_func
+
+    policy.set_path_policy(disable, cap)
+    try:
+        out = flash_attn_func(q, k, v, mask, None, dropout_p, causal, None, seed)
+        grads = torch.autograd.grad(out, (q, k, v), do)
+        torch.cuda.synchronize()
+    finally:
+        policy.set_path_policy(0, 0)
+    return [t.detach().clone() for t in (out,) + tuple(grads)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,dtype", BWD_CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_hand_placed_backward_bitwise_equals_general(b, hq, hkv, sq, sk, causal, dtype, policy):
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, 128, dtype)
+    # the forward from the general kernel in both arms, so dQ / dK / dV see the same O and LSE2
+    hp = _fwd_bwd(q, k, v, do, causal, policy=policy, disable=policy.PATH_FWD_HP)
+    gen = _fwd_bwd(q, k, v, do, causal, policy=policy,
+                   disable=policy.PATH_FWD_HP | policy.PATH_DQ_HP | policy.PATH_DKDV_HP)
+    for name, a, c in zip(("out", "dq", "dk", "dv"), hp, gen):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,dtype", BWD_CASES[:6], ids=lambda x: str(x).replace("torch.", ""))
+def test_hand_placed_forward_matches_pipelined(b, hq, hkv, sq, sk, causal, dtype, policy):
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from oracle.reference import attention_reference, lse2_reference
+
+    q, k, v, _ = generate_test_data(b, hq, hkv, sq, sk, 128, dtype)
+    res = {}
+    for tag, dis in (("hp", 0), ("pipe", policy.PATH_FWD_HP)):
+        policy.set_path_policy(dis, 0)
+        o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        res[tag] = (o.float(), lse[:, :, :sq].float())
+    policy.set_path_policy(0, 0)
+    ref = attention_reference(q, k, v, causal=causal).float()
+    pt = attention_reference(q, k, v, causal=causal, upcast=False, reorder_ops=True).float()
+    lref = lse2_reference(q, k, causal=causal)
+    fin = torch.isfinite(lref)
+    ept = (pt - ref).abs().max().item()
+    for tag, (o, lse) in res.items():
+        assert (o - ref).abs().max().item() <= 2 * ept + 5e-5, tag
+        assert torch.equal(torch.isfinite(lse), fin), tag
+        if fin.any():
+            assert (lse[fin] - lref[fin]).abs().max().item() <= 1e-3 * (1 + lref[fin].abs().max().item()), tag
+
+
+GRID_CASES = [
+    # b, hq, hkv, s, causal, dtype, varlen
+    (2, 8, 2, 1024, True, torch.bfloat16, False),
+    (2, 8, 8, 1024, False, torch.float16, False),
+    (3, 4, 2, 777, True, torch.bfloat16, True),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [2, 3])
+@pytest.mark.parametrize("b,hq,hkv,s,causal,dtype,varlen", GRID_CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_persistent_units_bitwise_equal_any_grid(b, hq, hkv, s, causal, dtype, varlen, cap, policy):
+    q, k, v, do = generate_test_data(b, hq, hkv, s, s, 128, dtype)
+    mask = generate_attention_mask(q) if varlen else None
+    full = _fwd_bwd(q, k, v, do, causal, mask, policy=policy)
+    capped = _fwd_bwd(q, k, v, do, causal, mask, policy=policy, cap=cap)
+    for name, a, c in zip(("out", "dq", "dk", "dv"), full, capped):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, c), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [0, 2])
+@pytest.mark.parametrize("causal", [True, False])
+def test_dropout_hand_placed_dq_multi_unit(causal, cap, policy):
+    """The hand-placed dropout dQ reads the forward's saved keep words; several units per workgroup
+    (cap 2) must give the dQ of the general kernel regenerating the keep bits with Philox."""
+    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from fa2_triton_amd.utils import dropout_mask_words
+
+    b, hq, hkv, s, p = 2, 4, 2, 1024, 0.2
+    q, k, v, do = generate_test_data(b, hq, hkv, s, s, 128, torch.bfloat16)
+    words = torch.empty(dropout_mask_words(b, hq, s, s), dtype=torch.int32, device="cuda")
+    o, lse, scale, seed = _flash_attn_forward(q, k, v, None, None, p, causal, None, 1234, dropout_mask=words)
+    policy.set_path_policy(0, cap)
+    hp = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=words)
+    policy.set_path_policy(policy.PATH_DQ_HP | policy.PATH_DKDV_HP, 0)
+    regen = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=None)
+    policy.set_path_policy(0, 0)
+    for name, a, c in zip(("dq", "dk", "dv"), hp[:3], regen[:3]):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
