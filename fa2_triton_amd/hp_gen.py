@@ -928,75 +928,90 @@ class FwdGen:
 # ----------------------------------------------------------------------------------------------
 # dK / dV (the backward's dominant kernel): dkdv_hp_kernel (csrc/dkdv_hp_kernel.h)
 #
+# Software-pipelined step (round 5): the step i of a wave runs, between two barriers,
+#   M 0-7    the last 8 dK MFMAs of step i-1 (dK^T += Q^T dS for rows 16-31; operands read before
+#            the barrier: the Q^T fragments in the row ring, the packed dS in registers), so the
+#            step opens with MFMAs while its first LDS reads are in flight;
+#   M 8-23   S(i+1) = Q(i+1) K^T into the other S register set (the NEXT step's scores);
+#   M 24-39  dP(i) = dO(i) V^T, seeded with the -delta rows;
+#   M 40-55  dV^T += dO(i)^T P(i);
+#   M 56-63  dK^T += Q(i)^T dS(i), rows 0-15.
+# so the exponentials of P(i) (whose S(i) the previous step computed) run beside M 0-47 and dS(i)
+# beside M 41-63 (round 4 ran S(i) first and waited for it: the exponentials crowded 16 gaps).
+#
 # Register map of the statement:
-#   v[0:31]     S[kb] accumulators, then P = exp2(acc scale log2 e - LSE2) in place
-#   v[32:63]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place, then
+#   v[0:63]     S[st][kb] (two sets by step parity): the next step's scores, then P = exp2(s scale
+#               log2 e - LSE2) in place
+#   v[64:95]    dP[kb] accumulators (start as -delta rows), then dS = P (dP - delta) in place, then
 #               in place the packed dS DSP[kb][sp] (B operands of dK^T += Q^T dS)
-#   v[64:79]    PP[kb][sp] packed P (B operand of dV^T += dO^T P)
-#   v[80:95]    row-fragment ring (Q then dO, A operands of S and dP), 4 slots
-#   v[96:115]   V fragment ring (B operands of dP), 5 slots
-#   v[116:131]  transposed fragment ring (dO^T then Q^T, A operands of dV^T and dK^T), 4 slots
-#   v[132:135]  mask bounds LO[kb], HI[kb] of a masked step
-#   v[136:151]  LSE2 of the 16 rows of this lane's registers (read per step from LDS)
+#   v[96:111]   PP[kb][sp] packed P (B operand of dV^T += dO^T P)
+#   v[112:127]  row-fragment ring, 4 slots: Q(i+1), dO(i), then the Q^T(i) fragments of rows 16-31
+#               for the next step's first MFMAs
+#   v[128:143]  V fragment ring (B operands of dP), 4 slots
+#   v[144:159]  transposed fragment ring (dO^T, then Q^T of rows 0-15), 4 slots
+#   v[160:167]  LSE2 of 8 of the lane's rows (rows of 16-row half sp, reloaded for sp = 1)
 #   a[0:127]    dV^T[kb][dt], a[128:255] dK^T[kb][dt]
 #   K fragments: compiler-placed "v" operands %[k0]..%[k15]
-# LDS (bytes from the workgroup's base): a ring of DK_NBUF = 3 step buffers (the step i + 2's
-# tiles are requested during step i): Q tile of buffer b at 16384 b, dO tile at 16384 b + 8192
-# (Tile<128, 32>), V rows of wave w at DK_V0 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of
-# buffer b at DK_ROWS + 256 b (+128).
-DK_NBUF = 3
+# LDS (bytes from the workgroup's base): a ring of DK_NBUF = 4 step buffers -- step i reads
+# buffers i and i + 1, its DMA fills buffer i + 3 (two steps of lead): Q tile of buffer b at
+# 16384 b, dO tile at 16384 b + 8192 (Tile<128, 32>), V rows of wave w at DK_V0 + 16384 w
+# (Tile<128, 64>), LSE2 / -delta rows of buffer b at DK_ROWS + 256 b (+128).
+DK_NBUF = 4
 DK_V0 = 16384 * DK_NBUF
 DK_ROWS = DK_V0 + 65536
 DK_LDS = DK_ROWS + 256 * DK_NBUF
-DK_AHEAD = DK_NBUF - 1  # steps of lead of a step's DMA
+DK_AHEAD = DK_NBUF - 1  # a step's DMA fills the buffer of the step DK_AHEAD later
 DK_VMEM = 4  # vector-memory ops of one step's DMA after its rows (the count each step end leaves)
-def DS(kb, i=None):
-    return rng("v", 16 * kb, 16) if i is None else f"v{16 * kb + i}"
+
+
+def DS(st, kb, i=None):
+    base = 32 * st + 16 * kb
+    return rng("v", base, 16) if i is None else f"v{base + i}"
 
 
 def DDP(kb, i=None):
-    return rng("v", 32 + 16 * kb, 16) if i is None else f"v{32 + 16 * kb + i}"
-
-
-def DPP(kb, sp, j=None):
-    base = 64 + (kb * 2 + sp) * 4
-    return rng("v", base, 4) if j is None else f"v{base + j}"
+    return rng("v", 64 + 16 * kb, 16) if i is None else f"v{64 + 16 * kb + i}"
 
 
 def DDSP(kb, sp, j=None):
-    """Packed dS of 16-row step sp, in place over dP[kb] (as QDSP): pack j of elements 8 sp ..
+    """Packed dS of 16-row half sp, in place over dP[kb] (as QDSP): pack j of elements 8 sp ..
     8 sp + 7 reads 2j, 2j + 1 and writes element j."""
-    base = 32 + 16 * kb + 8 * sp
+    base = 64 + 16 * kb + 8 * sp
     return rng("v", base, 4) if j is None else f"v{base + j}"
 
 
-def DRR(n):
-    return rng("v", 80 + 4 * (n % 4), 4)
+def DPP(kb, sp, j=None):
+    base = 96 + (kb * 2 + sp) * 4
+    return rng("v", base, 4) if j is None else f"v{base + j}"
 
 
-DVF_SLOTS = 5
-
-
-def DVF(n):
-    return rng("v", 96 + 4 * (n % DVF_SLOTS), 4)
-
-
-def DTR(n, half=None):
-    base = 116 + 4 * (n % 4)
+def DRR(slot, half=None):
+    base = 112 + 4 * (slot % 4)
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-DLO = ["v132", "v133"]
-DHI = ["v134", "v135"]
-DLSE0 = 136
+DVF_SLOTS = 4
+
+
+def DVF(n):
+    return rng("v", 128 + 4 * (n % DVF_SLOTS), 4)
+
+
+def DTR(slot, half=None):
+    base = 144 + 4 * (slot % 4)
+    return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
+
+
+DLSE0 = 160
 
 
 def DLSE(i):
-    """LSE2 of the row of register i (rows (i & 3) + 8 (i >> 2) + 4 hh of the step's tile)."""
-    return f"v{DLSE0 + i}"
+    """LSE2 of the row of register i (rows (i & 3) + 8 (i >> 2) + 4 hh of the step's tile); the
+    8 registers hold the rows of one half sp = i >> 3 at a time."""
+    return f"v{DLSE0 + (i & 7)}"
 
 
-DK_NVGPR = 152
+DK_NVGPR = 168
 
 
 def DDV(kb, dt):
@@ -1011,30 +1026,29 @@ def DDK(kb, dt):
 D_G = "s64"        # q-head index in the group
 D_IDX = "s65"      # step index within the head
 D_CM = "s66"       # first query row of the current tile
-D_PAR = "s67"      # buffer parity of the current step
-D_QD = "s[68:71]"  # descriptors of the next step's Q, dO, LSE2 and delta rows
+D_PAR = "s67"      # step phase i mod DK_NBUF (buffer of step i; S set = phase & 1)
+D_QD = "s[68:71]"  # descriptors of the requested step's Q, dO, LSE2 and delta rows
 D_OD = "s[72:75]"
 D_LD = "s[76:79]"
 D_DD = "s[80:83]"
-D_QP = ("s84", "s85")  # next step's Q tile address, dO tile address
+D_QP = ("s84", "s85")  # requested step's Q tile address, dO tile address
 D_OP = ("s86", "s87")
-D_LC = "s88"       # next step's LSE2 / delta byte offset from the row bases
-D_NM = "s89"       # next step's first query row
-D_LEFT = "s90"     # steps after the current one
-D_NMT = "s91"      # next step's tile index within its head
+D_LC = "s88"       # requested step's LSE2 / delta byte offset from the row bases
+D_NM = "s89"       # requested step's first query row
+D_LEFT = "s90"     # total steps - the requested step's index (> 0: it exists)
+D_NMT = "s91"      # requested step's tile index within its head
 D_M0 = "s92"
 D_T = "s93"
-D_EX = "s[94:95]"
+D_EX = "s[94:95]"  # exec save of the rows DMA; s94 also a temporary of single items
 D_MK = ["s[96:97]", "s[98:99]"]
-D_SGPR_CLOBBER = list(range(64, 100))
 
 
 class DkdvGen:
     """dK / dV: 4 waves x 64 keys (two 32-key blocks kb per wave, one wave per SIMD); per step
-    (32 query rows of one q-head) 64 MFMAs: S[kb] = Q K'^T (16), dP[kb] = dO V^T (16),
-    dV^T[kb] += dO^T P (16), dK^T[kb] += Q^T dS (16); every Q / dO / transposed fragment read from
-    LDS feeds both key blocks.  Same math as the reference's dK/dV loop
-    (/root/reference/src/backward/compute_dkdv.py:42-112) and dkdv_kernel."""
+    (32 query rows of one q-head) 64 MFMAs: S(i+1)[kb] = Q K'^T (16), dP(i)[kb] = dO V^T (16),
+    dV^T[kb] += dO^T P (16), dK^T[kb] += Q^T dS (16, 8 of them in the next step); every Q / dO /
+    transposed fragment read from LDS feeds both key blocks.  Same math as the reference's dK/dV
+    loop (/root/reference/src/backward/compute_dkdv.py:42-112) and dkdv_kernel."""
 
     def __init__(self, bf16, causal):
         self.bf16, self.causal = bf16, causal
@@ -1043,12 +1057,11 @@ class DkdvGen:
         self.e = Emitter()
 
     # -- pieces ----------------------------------------------------------------------------------
-    def row_read(self, par, n):
-        """Row fragment n of the step: n < 8 Q k-step n, else dO k-step n - 8 (buffer par)."""
-        ks = n % 8
-        imm = par * 16384 + (8192 if n >= 8 else 0) + (ks >> 1) * 2048
+    def row_read(self, buf, dout, ks):
+        """Row fragment ks (Q, or dO when dout) of buffer buf into ring slot ks % 4."""
+        imm = buf * 16384 + (8192 if dout else 0) + (ks >> 1) * 2048
         base = "%[qb1]" if ks & 1 else "%[qb0]"
-        d = DRR(n)
+        d = DRR(ks)
         self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
 
     def v_frag(self, n):
@@ -1059,45 +1072,50 @@ class DkdvGen:
         d = DVF(n)
         self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
 
-    def tr_read(self, par, n, half):
-        """Transposed fragment n (n < 8: dO^T, else Q^T) f = n % 8: sp = f >> 2, dt = f & 3."""
-        f = n % 8
+    def tr_read(self, buf, dout, f, half, dst):
+        """Half `half` of transposed fragment f (sp = f >> 2, dt = f & 3) of dO^T (dout) or Q^T of
+        buffer buf into the 2 registers dst."""
         sp, dt = f >> 2, f & 3
-        imm = par * 16384 + (0 if n >= 8 else 8192) + dt * 2048 + 16 * sp * 64
+        imm = buf * 16384 + (8192 if dout else 0) + dt * 2048 + 16 * sp * 64
         base = "%[tb]" if half else "%[ta]"
-        d = DTR(n, half)
-        self.e.ds_read(f"ds_read_b64_tr_b16 {d}, {base} offset:{imm}", d)
+        self.e.ds_read(f"ds_read_b64_tr_b16 {dst}, {base} offset:{imm}", dst)
 
-    def init_read(self, par, what, kb, g4):
-        """LSE2 (what 0) rows into the LSE registers, -delta (what 1) into dP[kb] (the dP
-        chain's initial accumulator): register group g4."""
-        imm = par * 256 + what * 128 + 32 * g4
-        d = rng("v", DLSE0 + 4 * g4, 4) if what == 0 else rng("v", 32 + 16 * kb + 4 * g4, 4)
+    def init_read(self, buf, what, kb, g4):
+        """LSE2 (what 0; g4 in the half's pair) rows into the LSE registers, -delta (what 1) into
+        dP[kb] (the dP chain's initial accumulator): register group g4."""
+        imm = buf * 256 + what * 128 + 32 * g4
+        d = rng("v", DLSE0 + 4 * (g4 & 1), 4) if what == 0 else rng("v", 64 + 16 * kb + 4 * g4, 4)
         self.e.ds_read(f"ds_read_b128 {d}, %[lb] offset:{imm}", d)
 
-    def descriptors(self):
-        """Descriptors of the next step's tiles from the cursors (range 0 when there is none)."""
+    def descriptors(self, part=None):
+        """Descriptors of the requested step's tiles from the cursors (range 0 when none); part
+        0: the ranges (D_T rows, s94 the rows' bytes), 1: Q and dO, 2: LSE2 and delta rows."""
         e = self.e
-        t2 = "s94"  # (D_EX, free until the rows' DMA)
-        e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
-        e.salu(f"s_cmp_gt_i32 {D_LEFT}, 0")
-        e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
-        e.salu(f"s_cselect_b32 {t2}, 128, 0")
-        for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
-            e.salu(f"s_mov_b32 s{d}, {p0}")
-            e.salu(f"s_and_b32 s{d + 1}, {p1}, 0xffff")
-            e.salu(f"s_mul_i32 s{d + 2}, {D_T}, {rb}")
-            e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
-        for base, d in (("lse", 76), ("dl", 80)):
-            e.salu(f"s_add_u32 s{d}, %[{base}lo], {D_LC}")
-            e.salu(f"s_addc_u32 s{d + 1}, %[{base}hi], 0")
-            e.salu(f"s_and_b32 s{d + 1}, s{d + 1}, 0xffff")
-            e.salu(f"s_mov_b32 s{d + 2}, {t2}")
-            e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+        t2 = "s94"  # (D_EX, free outside the rows' DMA)
+        if part in (None, 0):
+            e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
+            e.salu(f"s_cmp_gt_i32 {D_LEFT}, 0")
+            e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
+            e.salu(f"s_cselect_b32 {t2}, 128, 0")
+        if part in (None, 1):
+            for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
+                e.salu(f"s_mov_b32 s{d}, {p0}")
+                e.salu(f"s_and_b32 s{d + 1}, {p1}, 0xffff")
+                e.salu(f"s_mul_i32 s{d + 2}, {D_T}, {rb}")
+                e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+        if part in (None, 2):
+            for base, d in (("lse", 76), ("dl", 80)):
+                e.salu(f"s_add_u32 s{d}, %[{base}lo], {D_LC}")
+                e.salu(f"s_addc_u32 s{d + 1}, %[{base}hi], 0")
+                e.salu(f"s_and_b32 s{d + 1}, s{d + 1}, 0xffff")
+                e.salu(f"s_mov_b32 s{d + 2}, {t2}")
+                e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
 
     def advance_cursors(self, tag):
-        """Cursors to the step after the next one: one tile down, or the next head's last tile."""
+        """Cursors to the step after the requested one: one tile down, or the next head's last
+        tile; one request fewer left."""
         e = self.e
+        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
         e.salu(f"s_add_u32 {D_NMT}, {D_NMT}, 1")
         e.salu(f"s_cmp_eq_u32 {D_NMT}, %[nmt]")
         e.raw(f"s_cbranch_scc1 .Lhp%=_{tag}_wrap")
@@ -1118,26 +1136,17 @@ class DkdvGen:
         e.salu(f"s_add_u32 {D_LC}, {D_LC}, %[lwrap]")
         e.label(f".Lhp%=_{tag}_adv")
 
-    def dma_items(self, par, tag):
-        """The step's DMA (wave 0: the LSE2 / delta rows first; then the Q, dO pieces) of the
-        step DK_AHEAD later into buffer (par + DK_AHEAD) mod DK_NBUF, as (cost, emit) items; m0
-        is set one item ahead.  Every wave's last DK_VMEM vector-memory ops are its pieces."""
-        nb = (par + DK_AHEAD) % DK_NBUF
+    def dma_items(self, nb, tag):
+        """One step's request into buffer nb as (cost, emit) items: the descriptors, wave 0's
+        LSE2 / delta rows, the Q, dO pieces (m0 set one item ahead), then the cursors.  Every
+        wave's last DK_VMEM vector-memory ops are its pieces."""
         pieces = [("q", 0), ("q", 1), ("o", 0), ("o", 1)]
 
         def m0_of(w_, it):
             return nb * 16384 + (8192 if w_ == "o" else 0) + it * 4096
 
-        out = []
-        for n, (w_, it) in enumerate(pieces):
-            def f(n=n, w_=w_, it=it):
-                if n == 0:
-                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(w_, it)}", m0=True)
-                off = f"%[{'q' if w_ == 'q' else 'o'}off{it}]"
-                self.e.dma(f"buffer_load_dwordx4 {off}, {D_QD if w_ == 'q' else D_OD}, 0 offen lds")
-                if n + 1 < len(pieces):
-                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(*pieces[n + 1])}", m0=True)
-            out.append((16, f))
+        # (issue costs of scalar instructions are taken as 2 cycles each)
+        out = [(8, lambda: self.descriptors(0)), (16, lambda: self.descriptors(1)), (20, lambda: self.descriptors(2))]
 
         def rows(tag=tag):
             e = self.e
@@ -1151,117 +1160,158 @@ class DkdvGen:
             e.dma(f"buffer_load_dwordx4 %[lsoff], {D_DD}, 0 offen lds")
             e.salu(f"s_mov_b64 exec, {D_EX}")
             e.label(f".Lhp%=_{tag}_nl")
-        return [(16, rows)] + out
+        out.append((16, rows))
+        for n, (w_, it) in enumerate(pieces):
+            def f(n=n, w_=w_, it=it):
+                if n == 0:
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(w_, it)}", m0=True)
+                off = f"%[{'q' if w_ == 'q' else 'o'}off{it}]"
+                self.e.dma(f"buffer_load_dwordx4 {off}, {D_QD if w_ == 'q' else D_OD}, 0 offen lds")
+                if n + 1 < len(pieces):
+                    self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(*pieces[n + 1])}", m0=True)
+            out.append((16, f))
+        out.append((20, lambda: self.advance_cursors(tag)))
+        return out
 
-    def mask_elem(self, kb, i):
-        """P = LO[kb] <= o < HI[kb] ? P : 0 for the register i of key block kb (o = row offset)."""
+    def mask_elem(self, st, kb, i):
+        """P = lo[kb] <= CM + o < hi[kb] ? P : 0 for register i of key block kb (o = the row
+        offset of the register; lo, hi the lane's visible rows, minus 4 hh)."""
         e = self.e
         o = (i & 3) + 8 * (i >> 2)
-        r = DS(kb, i)
-        ma, mb = D_MK[i & 1], D_MK[(i & 1) ^ 1] if False else D_MK[i & 1]
-        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, {DLO[kb]}, {o}", None, [DLO[kb]])
-        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, {DHI[kb]}, {o}", None, [DHI[kb]])
+        r = DS(st, kb, i)
+        e.salu(f"s_add_u32 s94, {D_CM}, {o}")
+        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, %[lo{kb}], s94", None, [])
+        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, %[hi{kb}], s94", None, [])
         e.salu(f"s_and_b64 {D_MK[0]}, {D_MK[0]}, {D_MK[1]}")
         e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
 
+    def cvt(self, d, a, b):
+        self.e.valu(f"{self.cvtop} {d}, {a}, {b}", d, [a, b])
+
+    # -- MFMAs -----------------------------------------------------------------------------------
+    def mf_dk_tail(self, g):
+        """Straddled MFMA g (0-7): dK^T[kb][dt] += Q^T(rows 16-31, dt) dS[kb] rows 16-31 of the
+        previous step (Q^T fragment in row-ring slot dt)."""
+        dt, kb = g >> 1, g & 1
+        self.e.mfma(self.mop, DDK(kb, dt), DRR(dt), DDSP(kb, 1), DDK(kb, dt))
+
+    def mf_s(self, st, g):
+        """S(next)[kb] (set st) += Q(ks) K[kb](ks), g = 2 ks + kb."""
+        ks, kb = g >> 1, g & 1
+        self.e.mfma(self.mop, DS(st, kb), DRR(ks), f"%[k{kb * 8 + ks}]", "0" if ks == 0 else DS(st, kb))
+
     # -- one step --------------------------------------------------------------------------------
     def step(self, par, cls, tag):
+        """Step i with i mod DK_NBUF = par, class A (live, unmasked), B (live, masked) or D (no key
+        of the wave visible: only the straddled MFMAs, S(i+1) and the request)."""
         e = self.e
+        st = par & 1           # S / P set of step i; S(i+1) goes to 1 - st
+        nxt = (par + 1) % DK_NBUF
         live = cls in ("A", "B")
         masked = cls == "B"
-        self.descriptors()
-        dma = self.dma_items(par, tag)
-        if not live:
-            for _, f in dma:
-                f()
-        else:
-            if masked:
-                for kb in range(2):
-                    e.valu(f"v_subrev_u32 {DLO[kb]}, {D_CM}, %[lo{kb}]", DLO[kb], [])
-                    e.valu(f"v_subrev_u32 {DHI[kb]}, {D_CM}, %[hi{kb}]", DHI[kb], [])
-            g = GapScheduler(64)
-            # LSE2 rows (used by the exponentials), -delta rows into dP[kb] (before the dP chains)
-            for g4 in range(4):
-                g.add("init0", 4, -1, 10, lambda g4=g4: self.init_read(par, 0, 0, g4))
+        g = GapScheduler(64 if live else 24)
+        # Q(i+1) row fragments ks -> ring slot ks % 4 (after the slot's previous occupant's last
+        # MFMA: the straddled MFMAs 2 dt + kb, then S MFMAs 8 + 2 ks + kb)
+        for ks in range(8):
+            rel = 2 * ks + 1
+            g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(nxt, False, ks))
+        for n, (c, f) in enumerate(self.dma_items((par + DK_AHEAD) % DK_NBUF, tag)):
+            g.add("dma", c, 2 if live else 0, (42 if live else 14) + 3 * n, f)
+        if live:
+            # dO(i) row fragments ks (slot ks % 4, after the S MFMAs 2 ks + 17), dP at 24 + 2 ks
+            for ks in range(8):
+                rel = 2 * ks + 17
+                g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(par, True, ks))
+            # Q^T(i) fragments of rows 16-31 (f = 4 + dt) into row-ring slots dt, after the dP
+            # MFMAs that read the slot's dO fragment (2 dt + 33): the next step's first MFMAs
+            for dt in range(4):
+                for h in range(2):
+                    g.add("row", 4, 2 * dt + 33, 58,
+                          lambda dt=dt, h=h: self.tr_read(par, False, 4 + dt, h, DRR(dt, h)))
+            # V fragments n (slot n % 4): dP MFMA 24 + n
+            for n in range(16):
+                rel = -1 if n < DVF_SLOTS else 24 + n - DVF_SLOTS
+                g.add("vf", 4, rel, max(rel, 21 + n), lambda n=n: self.v_frag(n))
+            # dO^T fragments f (slot f % 4): dV MFMAs 40 + 2 f + kb; then Q^T rows 0-15 (slot f)
+            for f in range(8):
+                rel = -1 if f < 4 else 2 * f + 33
+                for h in range(2):
+                    g.add("tr", 4, rel, 2 * f + 37, lambda f=f, h=h: self.tr_read(par, True, f, h, DTR(f, h)))
+            for f in range(4):
+                for h in range(2):
+                    g.add("tr", 4, 2 * f + 49, 2 * f + 53, lambda f=f, h=h: self.tr_read(par, False, f, h, DTR(f, h)))
+            # -delta rows into dP[kb] (register groups g4; g4 = 2 holds the packed dS of rows 16-31
+            # that the straddled MFMAs 2 dt + kb read: after them)
             for kb in range(2):
                 for g4 in range(4):
-                    g.add("init1", 4, -1, 12, lambda kb=kb, g4=g4: self.init_read(par, 1, kb, g4))
-            # row fragments: Q (S phase) then dO (dP phase), 3 ahead; V fragments 3 ahead
-            for n in range(16):
-                mf = 2 * n  # first MFMA using it (S: 2 ks, dP: 16 + 2 ks)
-                rel = -1 if n < 3 else mf - 6
-                g.add("row", 4, rel, max(rel, mf - 4), lambda n=n: self.row_read(par, n))
-            for n in range(16):
-                mf = 16 + n
-                rel = -1 if n < DVF_SLOTS - 1 else mf - DVF_SLOTS + 1
-                g.add("vf", 4, rel, max(rel, mf - 3), lambda n=n: self.v_frag(n))
-            # exponentials (after the S chains), mask, P packs
+                    rel = 7 + kb if g4 == 2 else -1
+                    g.add("init1", 4, rel, 20, lambda kb=kb, g4=g4: self.init_read(par, 1, kb, g4))
+            # LSE2 of half sp = 0 at once, of sp = 1 once every sp = 0 exponent argument is done
+            for g4 in (0, 1):
+                g.add("lse", 4, -1, 1, lambda g4=g4: self.init_read(par, 0, 0, g4))
+            for g4 in (2, 3):
+                g.add("lse", 4, 19, 21, lambda g4=g4: self.init_read(par, 0, 0, g4))
+            # exponentials of P(i) (set st): P = exp2(s scale log2 e - LSE2), the scale in fp32;
+            # mask; packs PP[kb][sp] (dV MFMAs 40 + 8 sp + 2 dt + kb)
             for sp in range(2):
+                r0, r1 = (2, 18) if sp == 0 else (22, 44)
                 for kb in range(2):
-                    for i in range(8 * sp, 8 * sp + 8):
-                        r = DS(kb, i)
-                        # P = exp2(s scale log2 e - LSE2), the scale applied in fp32
-                        g.add(f"exp{kb}", 4, 19, 26 + 8 * sp,
+                    els = list(range(8 * sp, 8 * sp + 8))
+                    for k, i in enumerate(els):
+                        r = DS(st, kb, i)
+                        dl = r0 + ((r1 - r0 - 6) * (k + 1)) // 8
+                        g.add(f"exp{kb}", 4, r0, dl,
                               lambda r=r, i=i: e.valu(f"v_fma_f32 {r}, {r}, %[sc], -{DLSE(i)}", r, [r, DLSE(i)]))
-                        g.add(f"exp{kb}", 8, 19, 27 + 8 * sp,
-                              lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
+                        g.add(f"exp{kb}", 8, r0, dl + 1, lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
                         if masked:
-                            g.add(f"exp{kb}", 16, 19, 28 + 8 * sp, lambda kb=kb, i=i: self.mask_elem(kb, i))
+                            g.add(f"exp{kb}", 20, r0, dl + 2, lambda kb=kb, i=i: self.mask_elem(st, kb, i))
                     for j in range(4):
-                        g.add(f"exp{kb}", 4, 19, 29 + 8 * sp,
-                              lambda kb=kb, sp=sp, j=j: self.cvt(DPP(kb, sp, j), DS(kb, 8 * sp + 2 * j), DS(kb, 8 * sp + 2 * j + 1)))
-            # dS = P dP' after the dP chains, dS packs
+                        g.add(f"exp{kb}", 4, r0, (38 if sp == 0 else 46),
+                              lambda kb=kb, sp=sp, j=j: self.cvt(DPP(kb, sp, j), DS(st, kb, 8 * sp + 2 * j),
+                                                               DS(st, kb, 8 * sp + 2 * j + 1)))
+            # dS(i) = P dP' after the dP chains (last MFMA 39; 4 MFMAs for the result), packs in place; DSP[kb][0] for the
+            # MFMAs 56 + 2 dt + kb, DSP[kb][1] for the next step's first MFMAs
             for kb in range(2):
                 for sp in range(2):
+                    dl = 52 if sp == 0 else 61
                     for i in range(8 * sp, 8 * sp + 8):
-                        a_, b_ = DS(kb, i), DDP(kb, i)
-                        g.add(f"ds{kb}", 4, 35, 44 + 8 * sp, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
+                        a_, b_ = DS(st, kb, i), DDP(kb, i)
+                        g.add(f"ds{kb}", 4, 43, dl, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
                     for j in range(4):
-                        g.add(f"ds{kb}", 4, 35, 45 + 8 * sp,
+                        g.add(f"ds{kb}", 4, 43, dl + 1,
                               lambda kb=kb, sp=sp, j=j: self.cvt(DDSP(kb, sp, j), DDP(kb, 8 * sp + 2 * j), DDP(kb, 8 * sp + 2 * j + 1)))
-            # transposed fragments: dO^T (dV) then Q^T (dK), 3 ahead
-            for n in range(16):
-                mf = 32 + 2 * n
-                rel = max(0, mf - 6)
-                for h in range(2):
-                    g.add("tr", 4, rel, mf - 3, lambda n=n, h=h: self.tr_read(par, n, h))
-            for n, (c, f) in enumerate(dma):
-                if "dk_nodma" not in ABL:
-                    g.add("dma", c, 2, 40 + n, f)
-            if "dk_novalu" in ABL:
-                g.items = [it for it in g.items if not it["stream"].startswith(("exp", "ds"))]
+        else:
+            # no dS of this step: the next step's straddled MFMAs add zeros
+            for kb in range(2):
+                for j in range(4):
+                    r = DDSP(kb, 1, j)
+                    g.add("zero", 4, 7 + kb, 20, lambda r=r: e.valu(f"v_mov_b32 {r}, 0", r))
 
-            def mfma(i):
-                if i < 16:  # S[kb] += Q(ks) K[kb](ks)
-                    ks, kb = i >> 1, i & 1
-                    e.mfma(self.mop, DS(kb), DRR(ks), f"%[k{kb * 8 + ks}]", "0" if ks == 0 else DS(kb))
-                elif i < 32:  # dP[kb] += dO(ks) V[kb](ks)
-                    ks, kb = (i - 16) >> 1, i & 1
-                    e.mfma(self.mop, DDP(kb), DRR(8 + ks), DVF(2 * ks + kb), DDP(kb))
-                elif i < 48:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
-                    f, kb = (i - 32) >> 1, i & 1
-                    sp, dt = f >> 2, f & 3
-                    e.mfma(self.mop, DDV(kb, dt), DTR(f), DPP(kb, sp), DDV(kb, dt))
-                else:  # dK^T[kb][dt] += Q^T(sp, dt) dS[kb](sp)
-                    f, kb = (i - 48) >> 1, i & 1
-                    sp, dt = f >> 2, f & 3
-                    e.mfma(self.mop, DDK(kb, dt), DTR(8 + f), DDSP(kb, sp), DDK(kb, dt))
+        def mfma(m):
+            if m < 8:
+                self.mf_dk_tail(m)
+            elif m < 24:
+                self.mf_s(1 - st, m - 8)
+            elif m < 40:  # dP[kb] += dO(ks) V[kb](ks)
+                ks, kb = (m - 24) >> 1, m & 1
+                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), DDP(kb))
+            elif m < 56:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
+                f, kb = (m - 40) >> 1, m & 1
+                e.mfma(self.mop, DDV(kb, f & 3), DTR(f), DPP(kb, f >> 2), DDV(kb, f & 3))
+            else:  # dK^T[kb][dt] += Q^T(rows 0-15, dt) dS[kb](rows 0-15)
+                f, kb = (m - 56) >> 1, m & 1
+                e.mfma(self.mop, DDK(kb, f), DTR(f), DDSP(kb, 0), DDK(kb, f))
 
-            g.run(mfma, pre_budget=48)
-        self.advance_cursors(tag)
-        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
+        g.run(mfma, pre_budget=24)
         e.salu(f"s_sub_u32 {D_CM}, {D_CM}, 32")
-        e.salu(f"s_mov_b32 {D_PAR}, {(par + 1) % DK_NBUF}")
+        e.salu(f"s_mov_b32 {D_PAR}, {nxt}")
         e.drain_lds()
         if "dk_novm" not in ABL:
-            # the next step's tiles (requested one step ago) have landed; this step's stay in flight
+            # the next step's tiles (requested two steps ago) have landed; this step's stay in flight
             e.raw(f"s_waitcnt vmcnt({DK_VMEM})")
         if "dk_nobar" not in ABL:
             e.raw("s_barrier")
         e.reset()
-
-    def cvt(self, d, a, b):
-        self.e.valu(f"{self.cvtop} {d}, {a}, {b}", d, [a, b])
 
     def build(self):
         e = self.e
@@ -1270,7 +1320,13 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_M0}, m0")
         for r in range(256):
             e.valu(f"v_accvgpr_write_b32 a{r}, 0", f"a{r}", kind="accw")
-        # cursors: the step after step 0
+        # the first step's straddled MFMAs add zeros
+        for kb in range(2):
+            for j in range(4):
+                e.valu(f"v_mov_b32 {DDSP(kb, 1, j)}, 0", DDSP(kb, 1, j))
+        # cursors: step 0's tiles were requested before the statement (and waited for by the
+        # compiler's wait for the K fragments); steps 1 and 2 here, then the loop requests step
+        # i + 3 during step i
         e.salu(f"s_mov_b32 {D_QP[0]}, %[qlo]")
         e.salu(f"s_mov_b32 {D_QP[1]}, %[qhi]")
         e.salu(f"s_mov_b32 {D_OP[0]}, %[olo]")
@@ -1278,24 +1334,31 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_LC}, %[lc0]")
         e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
-        self.advance_cursors("init")
-        # step 0's tiles were requested before the statement (and waited for by the compiler's
-        # wait for the K fragments); step 1's into buffer 1 here, then the cursors go to step 2.
-        # D_LEFT = steps after the one requested next: at step i, total - 2 - i (signed)
         e.salu(f"s_mov_b32 {D_LEFT}, %[total]")
-        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
+        self.advance_cursors("init")  # -> step 1 (D_LEFT = total - 1)
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        self.descriptors()
-        for _, f in self.dma_items((1 - DK_AHEAD) % DK_NBUF, "pro"):
-            f()
-        self.advance_cursors("init2")
-        e.salu(f"s_sub_i32 {D_LEFT}, {D_LEFT}, 1")
+        for nb in (1, 2):
+            for _, f in self.dma_items(nb, f"pro{nb}"):
+                f()
         e.salu(f"s_mov_b32 {D_G}, 0")
         e.salu(f"s_mov_b32 {D_PAR}, 0")
         e.raw("s_barrier")
         e.reset()
         e.raw("s_cmp_eq_u32 %[total], 0")
         e.raw("s_cbranch_scc1 .Lhp%=_end")
+        # S(0) into set 0 from buffer 0
+        for ks in range(3):
+            self.row_read(0, False, ks)
+        for m in range(16):
+            ks = m >> 1
+            if m & 1 and ks + 3 < 8:
+                self.row_read(0, False, ks + 3)
+            self.mf_s(0, m)
+        e.drain_lds()
+        e.drain_mfma()
+        e.raw(f"s_waitcnt vmcnt({DK_VMEM})")  # step 1's tiles
+        e.raw("s_barrier")
+        e.reset()
         # head loop
         e.label(".Lhp%=_head")
         e.salu(f"s_mov_b32 {D_IDX}, 0")
@@ -1312,7 +1375,7 @@ class DkdvGen:
         e.label(".Lhp%=_clsD")
 
         def dispatch(cls):
-            # buffer parity D_PAR in 0 .. DK_NBUF - 1 -> the step body of that parity
+            # step phase D_PAR in 0 .. DK_NBUF - 1 -> the step body of that phase
             for par in range(DK_NBUF - 1):
                 e.raw(f"s_cmp_eq_u32 {D_PAR}, {par}")
                 e.raw(f"s_cbranch_scc1 .Lhp%=_{cls}{par}")
@@ -1334,6 +1397,9 @@ class DkdvGen:
         e.salu(f"s_add_u32 {D_G}, {D_G}, 1")
         e.raw(f"s_cmp_lt_u32 {D_G}, %[ng]")
         e.raw("s_cbranch_scc1 .Lhp%=_head")
+        # the last step's straddled MFMAs
+        for m in range(8):
+            self.mf_dk_tail(m)
         e.label(".Lhp%=_end")
         # every wave's (range-0) requests of the last steps have landed before any wave stages
         # its epilogue in the step buffers
