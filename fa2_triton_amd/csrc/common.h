@@ -452,8 +452,9 @@ struct BufStager {
   FA2_DEV static int max_rows(int64_t row_stride) {  // wave-uniform: kept in an SGPR
     return __builtin_amdgcn_readfirstlane((int)min((int64_t)0x7FFFFFFF, 0xFFFFFFFFll / (row_stride * 2)));
   }
-  FA2_DEV void piece(char* tile, i32x4 rsrc, int it) const {
-    if (kPieces % NTHREADS != 0 && wave * 64 >= kPieces) return;  // small tile: idle waves
+  // returns the saved m0: a token a caller can feed to a later statement to keep it behind the DMA
+  FA2_DEV uint32_t piece(char* tile, i32x4 rsrc, int it) const {
+    if (kPieces % NTHREADS != 0 && wave * 64 >= kPieces) return 0;  // small tile: idle waves
     const uint32_t lds = __builtin_amdgcn_readfirstlane(lds_addr(tile)) + wave_lds + it * NTHREADS * 16;
     uint32_t keep;
     asm volatile(
@@ -461,11 +462,14 @@ struct BufStager {
         : "=&s"(keep)
         : "v"(voff[it]), "s"(rsrc), "s"(lds)
         : "memory");
+    return keep;
   }
-  FA2_DEV void issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int max_rows) const {
+  FA2_DEV uint32_t issue(char* tile, const uint16_t* g, int64_t row_stride, int row0, int row_end, int max_rows) const {
     const i32x4 r = tile_rsrc(g, row_stride, row0, row_end, max_rows);
+    uint32_t tok = 0;
 #pragma unroll
-    for (int it = 0; it < kIters; ++it) piece(tile, r, it);
+    for (int it = 0; it < kIters; ++it) tok = piece(tile, r, it);
+    return tok;
   }
 };
 

@@ -64,6 +64,7 @@ class Emitter:
     M0_DMA = 2         # s_* writes m0 -> LDS-DMA
 
     def __init__(self):
+        self.drop = None   # development timing ablations: instructions matching it are not emitted
         self.out = []
         self.ws = 0
         self.wr = {}       # reg -> (ws, kind)
@@ -130,7 +131,9 @@ class Emitter:
                 break
             if r in self.rd_ab and kind != "ds":
                 need = max(need, self.MFMA_READ_WAR - (self.ws - self.rd_ab[r]))
-            if r in self.rd_c:
+            # (an MFMA writing a register an earlier MFMA read as C: ordered by the in-order
+            # matrix pipe, which reads C before any later MFMA's result lands)
+            if r in self.rd_c and kind != "mfma":
                 need = max(need, self.MFMA_C_WAR - (self.ws - self.rd_c[r]))
         self._pad(need)
 
@@ -153,6 +156,8 @@ class Emitter:
         self.n_mfma += 1
 
     def valu(self, text, dst, srcs=(), kind="valu"):
+        if self.drop and self.drop.search(text):
+            return
         wr = set()
         for d in ([dst] if isinstance(dst, str) else (dst or [])):
             wr |= set(_regs(d))
@@ -165,6 +170,8 @@ class Emitter:
         self._commit(kind, wr)
 
     def ds_read(self, text, dst, addr=None):
+        if self.drop and self.drop.search(text):
+            return
         wr = set(_regs(dst))
         self._need_lgkm(wr)
         self._hazards("ds", set(_regs(addr)) if addr else set(), wr)
@@ -172,6 +179,8 @@ class Emitter:
         self.ds.append(wr)
 
     def salu(self, text, m0=False):
+        if self.drop and self.drop.search(text) and not m0:
+            return
         self._line(text)
         if m0:
             self.wr["m0"] = (self.ws, "m0")
@@ -295,12 +304,18 @@ class GapScheduler:
 
     BUDGET = 24
 
-    def __init__(self, n):
+    def __init__(self, n, lds_cap=None):
+        """lds_cap: at most this much LDS read weight per gap (items added with lds = their weight,
+        e.g. 2 per 1 KiB ds_read_b128, 1 per 512 B ds_read_b64_tr_b16), unless at their
+        deadline: the four waves of a CU share 256 B/clk of LDS reads, and a burst of reads
+        queues behind itself (and a wave stalls at issue with 15 LDS operations outstanding)."""
         self.n = n
         self.items = []
+        self.lds_cap = lds_cap
 
-    def add(self, stream, cost, release, deadline, emit):
-        self.items.append(dict(stream=stream, cost=cost, rel=release, dl=deadline, emit=emit, seq=len(self.items)))
+    def add(self, stream, cost, release, deadline, emit, lds=False):
+        self.items.append(dict(stream=stream, cost=cost, rel=release, dl=deadline, emit=emit, seq=len(self.items),
+                               lds=lds))
 
     def run(self, mfma, pre_budget=0):
         pending = list(self.items)
@@ -317,8 +332,11 @@ class GapScheduler:
         tick = [0]
 
         def fill(g, budget):
+            nl = 0
+            cap = self.lds_cap
             while True:
-                el = [it for it in heads() if it["rel"] <= g]
+                el = [it for it in heads()
+                      if it["rel"] <= g and not (cap is not None and it["lds"] and nl + it["lds"] > cap and it["dl"] > g)]
                 if not el:
                     return
                 # earliest deadline first; among equals the stream served longest ago (two
@@ -336,6 +354,7 @@ class GapScheduler:
                 last_use[it["stream"]] = tick[0]
                 tick[0] += 1
                 budget -= it["cost"]
+                nl += it["lds"] or 0
 
         fill(-1, pre_budget)
         for g in range(self.n):
@@ -990,7 +1009,7 @@ def DRR(slot, half=None):
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-DVF_SLOTS = 4
+DVF_SLOTS = 5 if "dk_vf5" in ABL else 4
 
 
 def DVF(n):
@@ -1002,7 +1021,7 @@ def DTR(slot, half=None):
     return rng("v", base, 4) if half is None else rng("v", base + 2 * half, 2)
 
 
-DLSE0 = 160
+DLSE0 = 160 + (4 if "dk_vf5" in ABL else 0)
 
 
 def DLSE(i):
@@ -1011,7 +1030,7 @@ def DLSE(i):
     return f"v{DLSE0 + (i & 7)}"
 
 
-DK_NVGPR = 168
+DK_NVGPR = DLSE0 + 8
 
 
 def DDV(kb, dt):
@@ -1039,7 +1058,7 @@ D_LEFT = "s90"     # total steps - the requested step's index (> 0: it exists)
 D_NMT = "s91"      # requested step's tile index within its head
 D_M0 = "s92"
 D_T = "s93"
-D_EX = "s[94:95]"  # exec save of the rows DMA; s94 also a temporary of single items
+D_EX = "s[94:95]"  # exec save of the rows DMA; s94 also the rows' range (descriptor items 0 -> 2)
 D_MK = ["s[96:97]", "s[98:99]"]
 
 
@@ -1179,9 +1198,11 @@ class DkdvGen:
         e = self.e
         o = (i & 3) + 8 * (i >> 2)
         r = DS(st, kb, i)
-        e.salu(f"s_add_u32 s94, {D_CM}, {o}")
-        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, %[lo{kb}], s94", None, [])
-        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, %[hi{kb}], s94", None, [])
+        # the row in s98 (the second compare reads it before writing s[98:99]); not s94, which
+        # carries the rows' range from one descriptor item to the next
+        e.salu(f"s_add_u32 s98, {D_CM}, {o}")
+        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, %[lo{kb}], s98", None, [])
+        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, %[hi{kb}], s98", None, [])
         e.salu(f"s_and_b64 {D_MK[0]}, {D_MK[0]}, {D_MK[1]}")
         e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
 
@@ -1209,52 +1230,55 @@ class DkdvGen:
         nxt = (par + 1) % DK_NBUF
         live = cls in ("A", "B")
         masked = cls == "B"
-        g = GapScheduler(64 if live else 24)
+        g = GapScheduler(64 if live else 24, lds_cap=None if "dk_nocap" in ABL else 3)
         # Q(i+1) row fragments ks -> ring slot ks % 4 (after the slot's previous occupant's last
         # MFMA: the straddled MFMAs 2 dt + kb, then S MFMAs 8 + 2 ks + kb)
         for ks in range(8):
             rel = 2 * ks + 1
-            g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(nxt, False, ks))
+            g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(nxt, False, ks), lds=2)
         for n, (c, f) in enumerate(self.dma_items((par + DK_AHEAD) % DK_NBUF, tag)):
             g.add("dma", c, 2 if live else 0, (42 if live else 14) + 3 * n, f)
         if live:
             # dO(i) row fragments ks (slot ks % 4, after the S MFMAs 2 ks + 17), dP at 24 + 2 ks
             for ks in range(8):
                 rel = 2 * ks + 17
-                g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(par, True, ks))
+                g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(par, True, ks), lds=2)
             # Q^T(i) fragments of rows 16-31 (f = 4 + dt) into row-ring slots dt, after the dP
             # MFMAs that read the slot's dO fragment (2 dt + 33): the next step's first MFMAs
             for dt in range(4):
                 for h in range(2):
                     g.add("row", 4, 2 * dt + 33, 58,
-                          lambda dt=dt, h=h: self.tr_read(par, False, 4 + dt, h, DRR(dt, h)))
+                          lambda dt=dt, h=h: self.tr_read(par, False, 4 + dt, h, DRR(dt, h)), lds=1)
             # V fragments n (slot n % 4): dP MFMA 24 + n
             for n in range(16):
-                rel = -1 if n < DVF_SLOTS else 24 + n - DVF_SLOTS
-                g.add("vf", 4, rel, max(rel, 21 + n), lambda n=n: self.v_frag(n))
+                rel = 8 if n < DVF_SLOTS else 24 + n - DVF_SLOTS
+                g.add("vf", 4, rel, max(rel, 21 + n), lambda n=n: self.v_frag(n), lds=2)
             # dO^T fragments f (slot f % 4): dV MFMAs 40 + 2 f + kb; then Q^T rows 0-15 (slot f)
             for f in range(8):
-                rel = -1 if f < 4 else 2 * f + 33
+                rel = 0 if f < 4 else 2 * f + 33
                 for h in range(2):
-                    g.add("tr", 4, rel, 2 * f + 37, lambda f=f, h=h: self.tr_read(par, True, f, h, DTR(f, h)))
+                    g.add("tr", 4, rel, 2 * f + 37, lambda f=f, h=h: self.tr_read(par, True, f, h, DTR(f, h)), lds=1)
             for f in range(4):
                 for h in range(2):
-                    g.add("tr", 4, 2 * f + 49, 2 * f + 53, lambda f=f, h=h: self.tr_read(par, False, f, h, DTR(f, h)))
-            # -delta rows into dP[kb] (register groups g4; g4 = 2 holds the packed dS of rows 16-31
-            # that the straddled MFMAs 2 dt + kb read: after them)
-            for kb in range(2):
-                for g4 in range(4):
-                    rel = 7 + kb if g4 == 2 else -1
-                    g.add("init1", 4, rel, 20, lambda kb=kb, g4=g4: self.init_read(par, 1, kb, g4))
-            # LSE2 of half sp = 0 at once, of sp = 1 once every sp = 0 exponent argument is done
-            for g4 in (0, 1):
-                g.add("lse", 4, -1, 1, lambda g4=g4: self.init_read(par, 0, 0, g4))
+                    g.add("tr", 4, 2 * f + 49, 2 * f + 53, lambda f=f, h=h: self.tr_read(par, False, f, h, DTR(f, h)),
+                          lds=1)
+            # -delta rows into dP[1] only (register groups g4; g4 = 2 holds the packed dS of rows
+            # 16-31 that the straddled MFMAs 2 dt + 1 read: after them); the first dP MFMA of block
+            # 0 takes dP[1] as its C (before block 1's chain overwrites it), so both chains start
+            # from the one copy of the rows
+            for g4 in range(4):
+                g.add("init1", 4, 8 if g4 == 2 else 0, 20, lambda g4=g4: self.init_read(par, 1, 1, g4), lds=2)
+            # LSE2 of this step's half sp = 1 once every sp = 0 exponent argument is done; half
+            # sp = 0 of the NEXT step once every sp = 1 one is (its rows landed a step ago), so no
+            # exponential waits for an LDS read at a step start (round 5: that wait cost ~8 %)
             for g4 in (2, 3):
-                g.add("lse", 4, 19, 21, lambda g4=g4: self.init_read(par, 0, 0, g4))
+                g.add("lse", 4, 14, 18, lambda g4=g4: self.init_read(par, 0, 0, g4), lds=2)
+            for g4 in (0, 1):
+                g.add("lse", 4, 40, 58, lambda g4=g4: self.init_read(nxt, 0, 0, g4), lds=2)
             # exponentials of P(i) (set st): P = exp2(s scale log2 e - LSE2), the scale in fp32;
             # mask; packs PP[kb][sp] (dV MFMAs 40 + 8 sp + 2 dt + kb)
             for sp in range(2):
-                r0, r1 = (2, 18) if sp == 0 else (22, 44)
+                r0, r1 = (0, 18) if sp == 0 else (21, 44)
                 for kb in range(2):
                     els = list(range(8 * sp, 8 * sp + 8))
                     for k, i in enumerate(els):
@@ -1286,15 +1310,35 @@ class DkdvGen:
                 for j in range(4):
                     r = DDSP(kb, 1, j)
                     g.add("zero", 4, 7 + kb, 20, lambda r=r: e.valu(f"v_mov_b32 {r}, 0", r))
+            for g4 in (0, 1):  # the next step's LSE2 of half sp = 0
+                g.add("lse", 4, -1, 20, lambda g4=g4: self.init_read(nxt, 0, 0, g4), lds=2)
+
+        if "dk_novalu" in ABL:
+            g.items = [it for it in g.items if not it["stream"].startswith(("exp", "ds"))]
+        if "dk_nodma" in ABL:
+            g.items = [it for it in g.items if it["stream"] != "dma"]
+        if "dk_nolds" in ABL:
+            g.items = [it for it in g.items if it["stream"] not in ("row", "vf", "tr", "init1", "lse")]
+        if "dk_nolgkm" in ABL:
+            e.ds = []
+            e._need_lgkm = lambda regs: None
+        drops = {"dk_noexp": r"^v_exp", "dk_nocvt": r"^v_cvt_pk", "dk_notr": r"^ds_read_b64_tr",
+                 "dk_novf": r"%\[vb[01]\]", "dk_norow": r"^ds_read_b128 .*%\[qb[01]\]", "dk_noinit": r"%\[lb\]",
+                 "dk_nosalu": r"^s_(mov_b32 s(6[89]|7\d|8[0-3])|and_b32 s|mul_i32|add_u32 s(7[6-9]|8[0-3])|addc|sub_u32 s8[4-9]|subb|cselect|sub_i32)",
+                 "dk_nomul": r"^v_mul_f32", "dk_nofma": r"^v_fma_f32",
+                 "dk_nolse": r"%\[lb\] offset:(0|32|64|96|256|288|320|352|512|544|576|608|768|800|832|864)$",
+                 "dk_nodl": r"%\[lb\] offset:(128|160|192|224|384|416|448|480|640|672|704|736|896|928|960|992)$"}
+        pat = "|".join(v for k, v in drops.items() if k in ABL)
+        e.drop = re.compile(pat) if pat else None
 
         def mfma(m):
             if m < 8:
                 self.mf_dk_tail(m)
             elif m < 24:
                 self.mf_s(1 - st, m - 8)
-            elif m < 40:  # dP[kb] += dO(ks) V[kb](ks)
+            elif m < 40:  # dP[kb] += dO(ks) V[kb](ks), both chains seeded from dP[1]'s -delta rows
                 ks, kb = (m - 24) >> 1, m & 1
-                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), DDP(kb))
+                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), DDP(1) if ks == 0 else DDP(kb))
             elif m < 56:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
                 f, kb = (m - 40) >> 1, m & 1
                 e.mfma(self.mop, DDV(kb, f & 3), DTR(f), DPP(kb, f >> 2), DDV(kb, f & 3))
@@ -1303,6 +1347,9 @@ class DkdvGen:
                 e.mfma(self.mop, DDK(kb, f), DTR(f), DDSP(kb, 0), DDK(kb, f))
 
         g.run(mfma, pre_budget=24)
+        if "dk_nolgkm" in ABL:
+            e._need_lgkm = Emitter._need_lgkm.__get__(e)
+        e.drop = None
         e.salu(f"s_sub_u32 {D_CM}, {D_CM}, 32")
         e.salu(f"s_mov_b32 {D_PAR}, {nxt}")
         e.drain_lds()
@@ -1336,14 +1383,17 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_NMT}, 0")
         e.salu(f"s_mov_b32 {D_LEFT}, %[total]")
         self.advance_cursors("init")  # -> step 1 (D_LEFT = total - 1)
+        # this block's V rows, step-0 tiles and K fragments (requested before the statement, during
+        # the previous block's epilogue) have landed; every wave is past that epilogue, whose
+        # staging images sit in step buffers 2-3
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        e.raw("s_barrier")
+        e.reset()
         for nb in (1, 2):
             for _, f in self.dma_items(nb, f"pro{nb}"):
                 f()
         e.salu(f"s_mov_b32 {D_G}, 0")
         e.salu(f"s_mov_b32 {D_PAR}, 0")
-        e.raw("s_barrier")
-        e.reset()
         e.raw("s_cmp_eq_u32 %[total], 0")
         e.raw("s_cbranch_scc1 .Lhp%=_end")
         # S(0) into set 0 from buffer 0
@@ -1354,6 +1404,8 @@ class DkdvGen:
             if m & 1 and ks + 3 < 8:
                 self.row_read(0, False, ks + 3)
             self.mf_s(0, m)
+        for g4 in (0, 1):  # step 0's LSE2 of half sp = 0 (each step loads the next one's)
+            self.init_read(0, 0, 0, g4)
         e.drain_lds()
         e.drain_mfma()
         e.raw(f"s_waitcnt vmcnt({DK_VMEM})")  # step 1's tiles
@@ -1439,19 +1491,20 @@ FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
 
 def gen_read_dkdv():
     parts = ["// dV^T a[0:127], dK^T a[128:255] of key block KB -> registers (after the statement's final",
-             "// drain); one key block at a time keeps the epilogue within the register file",
+             "// drain); one key block at a time keeps the epilogue within the register file; tok: a",
+             "// value of the next block's requests (kept ahead of these reads by the data dependence)",
              "template <int KB>",
-             "FA2_DEV void dkdv_hp_read(f32x16 (&dv)[4], f32x16 (&dk)[4]);"]
+             "FA2_DEV void dkdv_hp_read(f32x16 (&dv)[4], f32x16 (&dk)[4], uint32_t tok);"]
     for kb in range(2):
         parts.append("template <>")
-        parts.append(f"FA2_DEV void dkdv_hp_read<{kb}>(f32x16 (&dv)[4], f32x16 (&dk)[4]) {{")
+        parts.append(f"FA2_DEV void dkdv_hp_read<{kb}>(f32x16 (&dv)[4], f32x16 (&dk)[4], uint32_t tok) {{")
         for which, base0 in (("dv", 0), ("dk", 128)):
             for dt in range(4):
                 base = base0 + (kb * 4 + dt) * 16
                 outs = ", ".join(f'"=v"({which}[{dt}][{i}])' for i in range(16))
                 body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
                 clob = ", ".join(f'"a{r}"' for r in range(256))
-                parts.append(f'  asm volatile("{body}" : {outs} : : {clob});')
+                parts.append(f'  asm volatile("{body}" : {outs} : "s"(tok) : {clob});')
         parts.append("}")
     return "\n".join(parts) + "\n"
 

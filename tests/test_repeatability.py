@@ -17,6 +17,9 @@ EXTRA = [
     (2, 8, 2, 1024, 1024, 128, False, True, torch.bfloat16),
     (2, 4, 4, 300, 700, 64, False, False, torch.float16),
     (1, 2, 1, 2048, 2048, 256, False, True, torch.bfloat16),
+    # causal D = 128 on the hand-placed kernels with several units per persistent workgroup
+    (4, 32, 8, 2048, 2048, 128, False, True, torch.bfloat16),
+    (2, 16, 16, 1536, 1536, 128, True, True, torch.float16),
 ]
 
 
