@@ -162,6 +162,90 @@ FA2_DEV int xcd_item(int L, int total) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + idx;
 }
 
+// The unit sequence of one workgroup of a persistent kernel (fwd_hp, dq_hp, dkdv_hp).  Work items
+// -- a causal pair of mirrored blocks (rep 0 = heavy, 1 = light) or one block -- are numbered
+// head-major, `per` items per head of n blocks; XCD x (workgroups L = x + 8 j) owns a contiguous
+// slice [start, end) in proportion to its W workgroups.
+//  * whole items (no pairs, or W odd): workgroup j runs items start + j + k W, an item's blocks
+//    back to back;
+//  * split pairs (pairs, W even): the W workgroups form W/2 slots of two, and in round k the two
+//    workgroups of slot s run the two blocks of item start + k W/2 + s side by side (rep =
+//    side ^ (k & 1)).  The XCD's workgroups then touch W/2 items at once -- half the heads of one
+//    pair per workgroup (cfg3: two heads' K / V, 4 MiB = one L2, instead of four) -- and a
+//    workgroup alternates heavy and light blocks (balanced over two rounds).  A self-mirrored
+//    middle item (one block) leaves its side-1 workgroup to the next round.
+// State is (item, rep, k); everything else is recomputed from the grid, so little stays live.
+struct PersistSched {
+  int item, rep, k;
+
+  struct Slice {
+    int start, end, W, j;
+  };
+  static FA2_DEV Slice slice(int T) {
+    // opaque copies: nothing of the schedule is hoisted out of a kernel's unit loop and kept live
+    // (in VGPRs, for the divisions) across its asm statement
+    int G = gridDim.x, L = blockIdx.x;
+    asm volatile("" : "+s"(G), "+s"(L), "+s"(T));
+    const int x = L & 7;
+    const int g8 = G >> 3, gr = G & 7;
+    const int cw0 = x * g8 + min(x, gr);
+    Slice s;
+    s.W = g8 + (x < gr ? 1 : 0);
+    s.j = L >> 3;
+    s.start = (int)((int64_t)T * cw0 / G);
+    s.end = (int)((int64_t)T * (cw0 + s.W) / G);
+    return s;
+  }
+  static FA2_DEV bool split(const Slice& s, bool pair) { return pair && s.W >= 2 && !(s.W & 1); }
+  static FA2_DEV int reps(int it, int n, int per, bool pair) {
+    const int m = it % per;
+    return pair && n - 1 - m != m ? 2 : 1;
+  }
+  FA2_DEV void place(const Slice& s) {
+    const int h = s.W >> 1, slot = s.j % h, side = s.j / h;
+    item = s.start + k * h + slot;
+    rep = side ^ (k & 1);
+  }
+  // the first unit; false: this workgroup has none
+  FA2_DEV bool first(int T, int n, int per, bool pair) {
+    const Slice s = slice(T);
+    k = 0;
+    if (split(s, pair)) {
+      place(s);
+      while (item < s.end && rep >= reps(item, n, per, pair)) {
+        ++k;
+        place(s);
+      }
+    } else {
+      item = s.start + s.j;
+      rep = 0;
+    }
+    uniform();
+    return item < s.end;
+  }
+  // advance to the next unit; false: none left
+  FA2_DEV bool next(int T, int n, int per, bool pair) {
+    const Slice s = slice(T);
+    if (split(s, pair)) {
+      do {
+        ++k;
+        place(s);
+      } while (item < s.end && rep >= reps(item, n, per, pair));
+    } else if (++rep >= reps(item, n, per, pair)) {
+      item += s.W;
+      rep = 0;
+    }
+    uniform();
+    return item < s.end;
+  }
+  // the state in SGPRs (the integer divisions run on the VALU)
+  FA2_DEV void uniform() {
+    item = __builtin_amdgcn_readfirstlane(item);
+    rep = __builtin_amdgcn_readfirstlane(rep);
+    k = __builtin_amdgcn_readfirstlane(k);
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // LDS tile layout ("d-tile major").  A tile of ROWS x DT 16-bit elements is stored as DT/32
 // sub-tiles of ROWS x 32 columns; each sub-tile row is 64 bytes (four 16-byte chunks) and
