@@ -1115,7 +1115,9 @@ class DkdvGen:
             e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
             e.salu(f"s_cmp_gt_i32 {D_LEFT}, 0")
             e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
-            e.salu(f"s_cselect_b32 {t2}, 128, 0")
+            # LSE2 / delta bytes of the rows below Lq (rows past it read as zeros)
+            e.salu(f"s_min_u32 {t2}, {D_T}, 32")
+            e.salu(f"s_lshl_b32 {t2}, {t2}, 2")
         if part in (None, 1):
             for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
                 e.salu(f"s_mov_b32 s{d}, {p0}")
@@ -1171,12 +1173,14 @@ class DkdvGen:
             e = self.e
             e.raw("s_cmp_eq_u32 %[w0], 0")
             e.raw(f"s_cbranch_scc0 .Lhp%=_{tag}_nl")
+            # one row per lane (lanes 0-31): the range ends exactly at the last row below Lq
             e.salu(f"s_mov_b64 {D_EX}, exec")
-            e.salu("s_mov_b64 exec, 0xff")
+            e.salu("s_mov_b32 exec_lo, -1")
+            e.salu("s_mov_b32 exec_hi, 0")
             e.salu(f"s_add_u32 m0, %[lbs], {nb * 256}", m0=True)
-            e.dma(f"buffer_load_dwordx4 %[lsoff], {D_LD}, 0 offen lds")
+            e.dma(f"buffer_load_dword %[lsoff], {D_LD}, 0 offen lds")
             e.salu(f"s_add_u32 m0, %[lbs], {nb * 256 + 128}", m0=True)
-            e.dma(f"buffer_load_dwordx4 %[lsoff], {D_DD}, 0 offen lds")
+            e.dma(f"buffer_load_dword %[lsoff], {D_DD}, 0 offen lds")
             e.salu(f"s_mov_b64 exec, {D_EX}")
             e.label(f".Lhp%=_{tag}_nl")
         out.append((16, rows))
@@ -1193,17 +1197,20 @@ class DkdvGen:
         return out
 
     def mask_elem(self, st, kb, i):
-        """P = lo[kb] <= CM + o < hi[kb] ? P : 0 for register i of key block kb (o = the row
-        offset of the register; lo, hi the lane's visible rows, minus 4 hh)."""
+        """Causal: P = row >= key - diag ? P : 0 for register i of key block kb, as
+        CM + o - kd[kb] >= lr (o = the row offset of the register, kd[kb] = the block's first key
+        - diag, lr = r32 - 4 hh).  No other mask: query rows past Lq read zero Q, dO, LSE2 and
+        delta (the descriptors' ranges), so P = 1 there multiplies zeros; keys past Lk only reach
+        their own dK / dV rows, which are not stored."""
+        if not self.causal:
+            return
         e = self.e
         o = (i & 3) + 8 * (i >> 2)
         r = DS(st, kb, i)
-        # the row in s98 (the second compare reads it before writing s[98:99]); not s94, which
-        # carries the rows' range from one descriptor item to the next
+        # s98: not s94, which carries the rows' range from one descriptor item to the next
         e.salu(f"s_add_u32 s98, {D_CM}, {o}")
-        e.valu(f"v_cmp_le_i32_e64 {D_MK[0]}, %[lo{kb}], s98", None, [])
-        e.valu(f"v_cmp_gt_i32_e64 {D_MK[1]}, %[hi{kb}], s98", None, [])
-        e.salu(f"s_and_b64 {D_MK[0]}, {D_MK[0]}, {D_MK[1]}")
+        e.salu(f"s_sub_u32 s98, s98, %[kd{kb}]")
+        e.valu(f"v_cmp_ge_i32_e64 {D_MK[0]}, s98, %[lr]", None, [])
         e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
 
     def cvt(self, d, a, b):
@@ -1287,8 +1294,8 @@ class DkdvGen:
                         g.add(f"exp{kb}", 4, r0, dl,
                               lambda r=r, i=i: e.valu(f"v_fma_f32 {r}, {r}, %[sc], -{DLSE(i)}", r, [r, DLSE(i)]))
                         g.add(f"exp{kb}", 8, r0, dl + 1, lambda r=r: e.valu(f"v_exp_f32 {r}, {r}", r, [r], kind="trans"))
-                        if masked:
-                            g.add(f"exp{kb}", 20, r0, dl + 2, lambda kb=kb, i=i: self.mask_elem(st, kb, i))
+                        if masked and self.causal:
+                            g.add(f"exp{kb}", 12, r0, dl + 2, lambda kb=kb, i=i: self.mask_elem(st, kb, i))
                     for j in range(4):
                         g.add(f"exp{kb}", 4, r0, (38 if sp == 0 else 46),
                               lambda kb=kb, sp=sp, j=j: self.cvt(DPP(kb, sp, j), DS(st, kb, 8 * sp + 2 * j),
@@ -1472,9 +1479,9 @@ def gen_dkdv_function(bf16, causal):
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
     sops = ["ng", "nmt", "total", "c0", "c01", "c012", "mlast", "lq", "qrb", "orb", "qtile", "otile", "qwrap",
             "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
-            "sc"]
-    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1", "ooff0", "ooff1", "lsoff",
-            "lo0", "lo1", "hi0", "hi1"]
+            "sc"] + (["kd0", "kd1"] if causal else [])
+    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1", "ooff0", "ooff1", "lsoff"] + \
+        (["lr"] if causal else [])
     src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
   asm volatile(
