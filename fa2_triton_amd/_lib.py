@@ -103,7 +103,7 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 7  # FA2_ABI_VERSION in include/fa2_amd.h
+ABI_VERSION = 8  # FA2_ABI_VERSION in include/fa2_amd.h
 
 EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes", "fa2_dropout_mask_bytes",
                     "fa2_cu_seqlens_from_mask", "fa2_set_path_policy",

@@ -176,7 +176,9 @@ int64_t fa2_bwd_dkv_workspace_bytes(const fa2_bwd_args* a) {
 
 int64_t fa2_dropout_mask_bytes(int32_t batch, int32_t heads_q, int32_t seqlen_q, int32_t seqlen_k) {
   if (batch < 1 || heads_q < 1 || seqlen_q < 1 || seqlen_k < 1) return 0;
-  return (int64_t)batch * heads_q * ((seqlen_q + 31) / 32) * ((seqlen_k + 31) / 32) * 128;
+  // + one tile of slack: the hand-placed dK/dV reads a wave's two key tiles as one 256-byte run,
+  // whose second tile lies past the end when the first is the last of the buffer (ABI 8)
+  return (int64_t)batch * heads_q * ((seqlen_q + 31) / 32) * ((seqlen_k + 31) / 32) * 128 + 128;
 }
 
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch, int32_t seqlen,

@@ -1556,10 +1556,11 @@ dq_done:
   }
   if ((stages & 2) && a.seqlen_k > 0) {
     const int ns = dkv_split(a);
-    if constexpr (DT == 128 && !BIAS && !DROPOUT && ALIGNED) {
-      // hand-placed one-wave-per-SIMD dK/dV (dkdv_hp_kernel.h) for D = 128 exactly
+    if constexpr (DT == 128 && !BIAS && ALIGNED) {
+      // hand-placed one-wave-per-SIMD dK/dV (dkdv_hp_kernel.h) for D = 128 exactly (dropout: with
+      // the forward's saved keep words)
       if (dkdv_hp_ok(a, true)) {
-        launch_dkdv_hp<BF16, CAUSAL>(a, ns, st);
+        launch_dkdv_hp<BF16, CAUSAL, DROPOUT>(a, ns, st);
         launch_dkv_reduce<BF16>(a, ns, st);
         return hipGetLastError();
       }

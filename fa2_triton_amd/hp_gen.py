@@ -1,25 +1,26 @@
-"""Generator of the hand-placed CDNA4 (gfx950) instruction streams of the forward kernel.
+"""Generator of the hand-placed CDNA4 (gfx950) instruction streams of the D = 128 kernels.
 
-The hot loop of `fwd_hp_kernel` (csrc/fwd_hp_kernel.h) is not compiler-scheduled: this module
-writes it as one inline-asm statement per (dtype, causal) variant into csrc/gen/fwd_hp_body.h
-(build.py calls `write_headers()` before compiling).  Every MFMA, exponential, LDS read, LDS-DMA
-piece and wait is placed by the tables below, in the spirit of cdna_hip_programming.md
-"4-wave, one-wave-per-SIMD, persistent structure": each 32-cycle MFMA gap carries a planned set
-of single-issue fillers (issue costs summed per gap, at most two exponentials), reads are
-counted (`s_waitcnt lgkmcnt(N)` computed from the exact LDS issue order), and every register
-hazard the hardware does not interlock (MFMA result -> vector read, vector write -> MFMA operand,
-transcendental -> use, permlane source) is padded by the `Emitter` from a register-state model,
-so the schedule tables only decide the ORDER.
+The hot loops of `fwd_hp_kernel`, `dq_hp_kernel` and `dkdv_hp_kernel` (csrc/*_hp_kernel.h) are
+not compiler-scheduled: this module writes each as one inline-asm statement per (dtype, causal,
+dropout) variant into csrc/gen/*_hp_body.h (build.py calls `write_headers()` before compiling).
+Every MFMA, exponential, LDS read, LDS-DMA piece and wait is placed by the tables below, in the
+spirit of cdna_hip_programming.md "4-wave, one-wave-per-SIMD, persistent structure": each
+32-cycle MFMA gap carries a planned set of single-issue fillers (issue costs summed per gap),
+reads are counted (`s_waitcnt lgkmcnt(N)` computed from the exact LDS issue order), and every
+register hazard the hardware does not interlock (MFMA result -> vector read, vector write -> MFMA
+operand, transcendental -> use, permlane source) is padded by the `Emitter` from a register-state
+model, so the schedule tables only decide the ORDER.
 
-Algorithm (same as the reference's compute_row_block, /root/reference/src/forward/
+Forward algorithm (same as the reference's compute_row_block, /root/reference/src/forward/
 compute_row_blocks.py:38-103, and fwd_pipe_kernel): per 64-key tile, S^T = K Q^T (swapped so the
 softmax row is one lane pair), online softmax in base 2 with defer-max (running max moved only
 when a row grows by more than 8), O^T += V^T P^T.  Differences of arrangement only:
-  * Q is pre-scaled by softmax_scale * log2(e) (rounded once to the input dtype) and the S chain
-    starts from -m_ref (the running reference max) as its initial accumulator, so the MFMA chain
-    yields the exponent argument z directly: no per-score multiply-add;
+  * the scale is applied in fp32, one fma per score: z = s (scale log2 e) - m_ref, as the
+    reference scales qk in fp32 (a pre-scaled-Q variant, whose LSE error exceeds the tests'
+    tolerance, exists only in FA2_HP_DEV development builds: `exact=False`);
   * the row sums of P are added in the PV phase (where the VALU has room), the exponentials of a
     tile ride on the next tile's QK^T MFMAs.
+The dQ (DqGen) and dK / dV (DkdvGen) streams are described at their classes.
 """
 import os
 import re
@@ -1031,6 +1032,23 @@ def DLSE(i):
 
 
 DK_NVGPR = DLSE0 + 8
+# dropout (the forward's saved keep words, DkdvGen(dropout=True)):
+#   DKM[kb]   the lane's keep column of key block kb (bit (i & 3) + 8 (i >> 2) = register i's row)
+#   DTM[kb]   temporary of key block kb: the P packs' masking, then the dS keep factors
+#   -delta of row group g4 (rows 8 g4 + 4 hh ..) in V fragment ring slot g4 (the ring is free from
+#   the dP MFMA that last reads a slot to the next step's first V fragment read)
+DKM = [f"v{DK_NVGPR}", f"v{DK_NVGPR + 1}"]
+DTM = [f"v{DK_NVGPR + 2}", f"v{DK_NVGPR + 3}"]
+DK_NVGPR_DROP = DK_NVGPR + 4
+D_MC = "s99"       # dropout: byte offset of the requested step's keep words from the wave's base
+DK_W0 = DK_LDS     # dropout: keep words of buffer b, wave w at DK_W0 + 1024 b + 256 w (64 dwords)
+DK_LDS_DROP = DK_W0 + 1024 * DK_NBUF
+
+
+def DDEL(g4, j=None):
+    base = 128 + 4 * g4
+    return rng("v", base, 4) if j is None else f"v{base + j}"
+
 
 
 def DDV(kb, dt):
@@ -1069,8 +1087,9 @@ class DkdvGen:
     transposed fragment read from LDS feeds both key blocks.  Same math as the reference's dK/dV
     loop (/root/reference/src/backward/compute_dkdv.py:42-112) and dkdv_kernel."""
 
-    def __init__(self, bf16, causal):
-        self.bf16, self.causal = bf16, causal
+    def __init__(self, bf16, causal, dropout=False):
+        self.bf16, self.causal, self.dropout = bf16, causal, dropout
+        assert not (dropout and DVF_SLOTS != 4), "the dropout -delta rows use the V ring's 4 slots"
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
@@ -1118,8 +1137,13 @@ class DkdvGen:
             # LSE2 / delta bytes of the rows below Lq (rows past it read as zeros)
             e.salu(f"s_min_u32 {t2}, {D_T}, 32")
             e.salu(f"s_lshl_b32 {t2}, {t2}, 2")
+            if self.dropout:  # lsoff = sb + DK_W0 + 256 w + 4 lane (w = 0 here): the range
+                # starts there (lbs = sb + DK_ROWS)
+                e.salu(f"s_add_u32 {t2}, {t2}, %[lbs]")
+                e.salu(f"s_add_u32 {t2}, {t2}, {DK_W0 - DK_ROWS}")
         if part in (None, 1):
-            for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, "%[orb]", 72)):
+            orb = "%[qrb]" if self.dropout else "%[orb]"  # (dropout: one row stride)
+            for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, orb, 72)):
                 e.salu(f"s_mov_b32 s{d}, {p0}")
                 e.salu(f"s_and_b32 s{d + 1}, {p1}, 0xffff")
                 e.salu(f"s_mul_i32 s{d + 2}, {D_T}, {rb}")
@@ -1141,11 +1165,16 @@ class DkdvGen:
         e.salu(f"s_cmp_eq_u32 {D_NMT}, %[nmt]")
         e.raw(f"s_cbranch_scc1 .Lhp%=_{tag}_wrap")
         e.salu(f"s_sub_u32 {D_NM}, {D_NM}, 32")
-        e.salu(f"s_sub_u32 {D_QP[0]}, {D_QP[0]}, %[qtile]")
+        # one tile = 32 rows (D_T: free once the step's descriptors are built)
+        e.salu(f"s_lshl_b32 {D_T}, %[qrb], 5")
+        e.salu(f"s_sub_u32 {D_QP[0]}, {D_QP[0]}, {D_T}")
         e.salu(f"s_subb_u32 {D_QP[1]}, {D_QP[1]}, 0")
-        e.salu(f"s_sub_u32 {D_OP[0]}, {D_OP[0]}, %[otile]")
+        e.salu(f"s_lshl_b32 {D_T}, {'%[qrb]' if self.dropout else '%[orb]'}, 5")
+        e.salu(f"s_sub_u32 {D_OP[0]}, {D_OP[0]}, {D_T}")
         e.salu(f"s_subb_u32 {D_OP[1]}, {D_OP[1]}, 0")
         e.salu(f"s_sub_u32 {D_LC}, {D_LC}, 128")
+        if self.dropout:
+            e.salu(f"s_sub_u32 {D_MC}, {D_MC}, %[mstep]")
         e.raw(f"s_branch .Lhp%=_{tag}_adv")
         e.label(f".Lhp%=_{tag}_wrap")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
@@ -1155,6 +1184,8 @@ class DkdvGen:
         e.salu(f"s_add_u32 {D_OP[0]}, {D_OP[0]}, %[owrap]")
         e.salu(f"s_addc_u32 {D_OP[1]}, {D_OP[1]}, 0")
         e.salu(f"s_add_u32 {D_LC}, {D_LC}, %[lwrap]")
+        if self.dropout:
+            e.salu(f"s_add_u32 {D_MC}, {D_MC}, %[mwrap]")
         e.label(f".Lhp%=_{tag}_adv")
 
     def dma_items(self, nb, tag):
@@ -1184,17 +1215,87 @@ class DkdvGen:
             e.salu(f"s_mov_b64 exec, {D_EX}")
             e.label(f".Lhp%=_{tag}_nl")
         out.append((16, rows))
+        if self.dropout:
+            def words(nb=nb):
+                # this wave's 64 keep words of the requested step (rows of the tile, key tiles
+                # kt0, kt0 + 1: one word per lane); D_LD is free again after the rows
+                e = self.e
+                e.salu("s_mov_b32 s76, %[mlo]")
+                e.salu("s_mov_b32 s77, %[mhi]")
+                e.salu("s_mov_b32 s79, 0x20000")
+                # m0 = sb + DK_W0 + 1024 nb + 256 w
+                e.salu("s_lshl_b32 s78, %[w0], 8")
+                e.salu(f"s_add_u32 s78, s78, %[lbs]")
+                e.salu(f"s_add_u32 m0, s78, {DK_W0 - DK_ROWS + nb * 1024}", m0=True)
+                e.salu("s_mov_b32 s78, -1")
+                e.dma(f"buffer_load_dword %[lsoff], s[76:79], {D_MC} offen lds")
+            out.append((16, words))
         for n, (w_, it) in enumerate(pieces):
             def f(n=n, w_=w_, it=it):
                 if n == 0:
                     self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(w_, it)}", m0=True)
-                off = f"%[{'q' if w_ == 'q' else 'o'}off{it}]"
+                off = f"%[{'q' if w_ == 'q' or self.dropout else 'o'}off{it}]"
                 self.e.dma(f"buffer_load_dwordx4 {off}, {D_QD if w_ == 'q' else D_OD}, 0 offen lds")
                 if n + 1 < len(pieces):
                     self.e.salu(f"s_add_u32 m0, %[mlds], {m0_of(*pieces[n + 1])}", m0=True)
             out.append((16, f))
         out.append((20, lambda: self.advance_cursors(tag)))
         return out
+
+    def keep_items(self, par, g):
+        """Dropout: this step's keep words (buffer par: lane (r32, hh) holds row r32 of key tile
+        hh) -> DKM[kb] = the lane's column of key block kb (bit r = row r; the hh = 1 lanes shifted
+        by 4 so bit (i & 3) + 8 (i >> 2) is register i's row), as dkdv_kernel's transpose32_lanes:
+        five ds_swizzle xor stages within each 32-lane half (the lane-dependent halves of a stage
+        under exec masks), then one v_permlane32_swap hands each half the other key block."""
+        e = self.e
+        m0_, m1_ = DKM
+        g.add("tp", 4, -1, 0, lambda: e.ds_read(f"ds_read_b32 {m0_}, %[lsoff] offset:{1024 * par}", m0_),
+              lds=1)
+        masks = {16: 0x0000FFFF, 8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+        for n, J in enumerate((16, 8, 4, 2, 1)):
+            def sw(J=J):
+                e._need_lgkm({m0_})
+                e.ds_read(f"ds_swizzle_b32 {m1_}, {m0_} offset:{0x1F | (J << 10)}", m1_)
+
+            def stage(J=J):
+                e._need_lgkm({m1_})
+                e.salu(f"s_mov_b32 s98, {hex(masks[J])}")
+                # lanes with lane bit J clear: x = (x & m) | (y << J & ~m)
+                e.salu("s_mov_b32 exec_lo, s98")
+                e.salu("s_mov_b32 exec_hi, s98")
+                e.valu(f"v_lshlrev_b32 {m1_}, {J}, {m1_}", m1_, [m1_])
+                e.valu(f"v_bfi_b32 {m0_}, s98, {m0_}, {m1_}", m0_, [m0_, m1_])
+                # lanes with it set: x = (y >> J & m) | (x & ~m)
+                e.salu("s_not_b32 exec_lo, s98")
+                e.salu("s_not_b32 exec_hi, s98")
+                e.valu(f"v_lshrrev_b32 {m1_}, {J}, {m1_}", m1_, [m1_])
+                e.valu(f"v_bfi_b32 {m0_}, s98, {m1_}, {m0_}", m0_, [m0_, m1_])
+                e.salu("s_mov_b64 exec, -1")
+            g.add("tp", 4, 2 * n, 2 * n + 2, sw, lds=1)
+            g.add("tp", 20, 2 * n + 1, 2 * n + 3, stage)
+
+        def fin():
+            e.valu(f"v_mov_b32 {m1_}, {m0_}", m1_, [m0_])
+            e.valu(f"v_permlane32_swap_b32 {m0_}, {m1_}", [m0_, m1_], [m0_, m1_], kind="perm")
+            e.salu("s_mov_b32 exec_lo, 0")
+            e.valu(f"v_lshrrev_b32 {m0_}, 4, {m0_}", m0_, [m0_])
+            e.valu(f"v_lshrrev_b32 {m1_}, 4, {m1_}", m1_, [m1_])
+            e.salu("s_mov_b64 exec, -1")
+        g.add("tp", 20, 10, 12, fin)
+
+    def pack_keep(self, kb, sp, j):
+        """Dropout: zero the halves of the P pack PP[kb][sp][j] whose element the forward dropped
+        (dV is scaled by 1 / (1 - p) once, in the epilogue)."""
+        e = self.e
+        pp, t = DPP(kb, sp, j), DTM[kb]
+        for h, a in enumerate((8 * sp + 2 * j, 8 * sp + 2 * j + 1)):
+            o = (a & 3) + 8 * (a >> 2)
+            e.valu(f"v_bfe_i32 {t}, {DKM[kb]}, {o}, 1", t, [DKM[kb]])
+            # (SDWA writes the low 16 bits of the result to the selected word: select the same word
+            # of both sources; bench_micro/sdwa_test.hip pins this on the hardware)
+            e.valu(f"v_and_b32_sdwa {pp}, {t}, {pp} dst_sel:WORD_{h} dst_unused:UNUSED_PRESERVE src0_sel:WORD_{h} "
+                   f"src1_sel:WORD_{h}", pp, [t, pp])
 
     def mask_elem(self, st, kb, i):
         """Causal: P = row >= key - diag ? P : 0 for register i of key block kb, as
@@ -1209,7 +1310,9 @@ class DkdvGen:
         r = DS(st, kb, i)
         # s98: not s94, which carries the rows' range from one descriptor item to the next
         e.salu(f"s_add_u32 s98, {D_CM}, {o}")
-        e.salu(f"s_sub_u32 s98, s98, %[kd{kb}]")
+        e.salu(f"s_sub_u32 s98, s98, %[kd0]")
+        if kb:
+            e.salu("s_sub_u32 s98, s98, 32")
         e.valu(f"v_cmp_ge_i32_e64 {D_MK[0]}, s98, %[lr]", None, [])
         e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
 
@@ -1273,8 +1376,18 @@ class DkdvGen:
             # 16-31 that the straddled MFMAs 2 dt + 1 read: after them); the first dP MFMA of block
             # 0 takes dP[1] as its C (before block 1's chain overwrites it), so both chains start
             # from the one copy of the rows
-            for g4 in range(4):
-                g.add("init1", 4, 8 if g4 == 2 else 0, 20, lambda g4=g4: self.init_read(par, 1, 1, g4), lds=2)
+            if not self.dropout:
+                for g4 in range(4):
+                    g.add("init1", 4, 8 if g4 == 2 else 0, 20, lambda g4=g4: self.init_read(par, 1, 1, g4), lds=2)
+            else:
+                # -delta rows (group g4) for dS = P (dP kp - delta), into V ring slot g4 once the
+                # dP MFMA 36 + g4 has read it
+                for g4 in range(4):
+                    d = DDEL(g4)
+                    rel, dl = 36 + g4, 41 + g4
+                    g.add("dl", 4, rel, dl, lambda g4=g4, d=d: self.e.ds_read(
+                        f"ds_read_b128 {d}, %[lb] offset:{par * 256 + 128 + 32 * g4}", d), lds=2)
+                self.keep_items(par, g)
             # LSE2 of this step's half sp = 1 once every sp = 0 exponent argument is done; half
             # sp = 0 of the NEXT step once every sp = 1 one is (its rows landed a step ago), so no
             # exponential waits for an LDS read at a step start (round 5: that wait cost ~8 %)
@@ -1297,12 +1410,37 @@ class DkdvGen:
                         if masked and self.causal:
                             g.add(f"exp{kb}", 12, r0, dl + 2, lambda kb=kb, i=i: self.mask_elem(st, kb, i))
                     for j in range(4):
-                        g.add(f"exp{kb}", 4, r0, (38 if sp == 0 else 46),
+                        g.add(f"exp{kb}", 4, r0, (38 if sp == 0 else (42 if self.dropout else 46)),
                               lambda kb=kb, sp=sp, j=j: self.cvt(DPP(kb, sp, j), DS(st, kb, 8 * sp + 2 * j),
                                                                DS(st, kb, 8 * sp + 2 * j + 1)))
+                        if self.dropout:  # (the keep columns are ready after the transposition;
+                            # DTM[kb] is the dS side's from MFMA 43 on)
+                            g.add(f"exp{kb}", 16, max(r0, 13), (38 if sp == 0 else 42),
+                                  lambda kb=kb, sp=sp, j=j: self.pack_keep(kb, sp, j))
             # dS(i) = P dP' after the dP chains (last MFMA 39; 4 MFMAs for the result), packs in place; DSP[kb][0] for the
             # MFMAs 56 + 2 dt + kb, DSP[kb][1] for the next step's first MFMAs
             for kb in range(2):
+                if self.dropout:
+                    # dS = P (dP kp - delta), kp = keep ? 1 / (1 - p) : 0 (bit for bit dkdv_kernel's
+                    # pr * (dp * kp + d4)); by row group g4, packs j of the group right after it
+                    for g4 in range(4):
+                        sp, dl = g4 >> 1, (50, 53, 58, 61)[g4]
+                        for i in range(4 * g4, 4 * g4 + 4):
+                            a_, b_, t_, d_ = DS(st, kb, i), DDP(kb, i), DTM[kb], DDEL(g4, i & 3)
+                            o = (i & 3) + 8 * (i >> 2)
+
+                            def dsd(a_=a_, b_=b_, t_=t_, d_=d_, o=o, kb=kb):
+                                e.valu(f"v_bfe_i32 {t_}, {DKM[kb]}, {o}, 1", t_, [DKM[kb]])
+                                e.valu(f"v_and_b32 {t_}, %[dscb], {t_}", t_, [t_])
+                                e.valu(f"v_fma_f32 {b_}, {b_}, {t_}, {d_}", b_, [b_, t_, d_])
+                            g.add(f"ds{kb}", 12, 43, dl, dsd)
+                            g.add(f"ds{kb}", 4, 43, dl,
+                                  lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
+                        for j in (2 * (g4 & 1), 2 * (g4 & 1) + 1):
+                            g.add(f"ds{kb}", 4, 43, dl + 1,
+                                  lambda kb=kb, sp=sp, j=j: self.cvt(DDSP(kb, sp, j), DDP(kb, 8 * sp + 2 * j),
+                                                                   DDP(kb, 8 * sp + 2 * j + 1)))
+                    continue
                 for sp in range(2):
                     dl = 52 if sp == 0 else 61
                     for i in range(8 * sp, 8 * sp + 8):
@@ -1345,7 +1483,8 @@ class DkdvGen:
                 self.mf_s(1 - st, m - 8)
             elif m < 40:  # dP[kb] += dO(ks) V[kb](ks), both chains seeded from dP[1]'s -delta rows
                 ks, kb = (m - 24) >> 1, m & 1
-                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), DDP(1) if ks == 0 else DDP(kb))
+                c = ("0" if self.dropout else DDP(1)) if ks == 0 else DDP(kb)
+                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), c)
             elif m < 56:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
                 f, kb = (m - 40) >> 1, m & 1
                 e.mfma(self.mop, DDV(kb, f & 3), DTR(f), DPP(kb, f >> 2), DDV(kb, f & 3))
@@ -1388,7 +1527,10 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_LC}, %[lc0]")
         e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
-        e.salu(f"s_mov_b32 {D_LEFT}, %[total]")
+        e.salu(f"s_mul_i32 {D_LEFT}, %[ng], %[nmt]")  # the block's steps
+        if self.dropout:  # step 0's keep words: mstep (nmt - 1)
+            e.salu(f"s_sub_u32 {D_MC}, %[nmt], 1")
+            e.salu(f"s_mul_i32 {D_MC}, {D_MC}, %[mstep]")
         self.advance_cursors("init")  # -> step 1 (D_LEFT = total - 1)
         # this block's V rows, step-0 tiles and K fragments (requested before the statement, during
         # the previous block's epilogue) have landed; every wave is past that epilogue, whose
@@ -1401,7 +1543,10 @@ class DkdvGen:
                 f()
         e.salu(f"s_mov_b32 {D_G}, 0")
         e.salu(f"s_mov_b32 {D_PAR}, 0")
-        e.raw("s_cmp_eq_u32 %[total], 0")
+        # no step at all (ng nmt = 0; D_G = 0 here)
+        e.raw(f"s_cmp_eq_u32 {D_G}, %[ng]")
+        e.raw("s_cbranch_scc1 .Lhp%=_end")
+        e.raw("s_cmp_eq_u32 %[nmt], 0")
         e.raw("s_cbranch_scc1 .Lhp%=_end")
         # S(0) into set 0 from buffer 0
         for ks in range(3):
@@ -1470,18 +1615,18 @@ class DkdvGen:
         return e.out
 
 
-def gen_dkdv_function(bf16, causal):
-    g = DkdvGen(bf16, causal)
+def gen_dkdv_function(bf16, causal, dropout=False):
+    g = DkdvGen(bf16, causal, dropout)
     lines = g.build()
-    name = f"dkdv_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}"
-    clob = [f'"v{i}"' for i in range(DK_NVGPR)] + [f'"a{i}"' for i in range(256)] + \
+    name = f"dkdv_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_drop' if dropout else ''}"
+    clob = [f'"v{i}"' for i in range(DK_NVGPR_DROP if dropout else DK_NVGPR)] + [f'"a{i}"' for i in range(256)] + \
            [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
-    sops = ["ng", "nmt", "total", "c0", "c01", "c012", "mlast", "lq", "qrb", "orb", "qtile", "otile", "qwrap",
+    sops = ["ng", "nmt", "c0", "c01", "c012", "mlast", "lq", "qrb"] + ([] if dropout else ["orb"]) + ["qwrap",
             "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
-            "sc"] + (["kd0", "kd1"] if causal else [])
-    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1", "ooff0", "ooff1", "lsoff"] + \
-        (["lr"] if causal else [])
+            "sc"] + (["kd0"] if causal else []) + (["mlo", "mhi", "mstep", "mwrap"] if dropout else [])
+    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1"] + ([] if dropout else ["ooff0", "ooff1"]) + \
+        ["lsoff"] + (["lr"] if causal else []) + (["dscb"] if dropout else [])
     src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
   asm volatile(
@@ -2051,7 +2196,8 @@ def write_headers():
     out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
     for bf16 in (True, False):
         for causal in (True, False):
-            out.append(gen_dkdv_function(bf16, causal))
+            for dropout in (False, True):
+                out.append(gen_dkdv_function(bf16, causal, dropout))
     out.append(gen_read_dkdv())
     out.append("}  // namespace fa2\n")
     paths.append(_write(os.path.join(GEN, "dkdv_hp_body.h"), "\n".join(out)))

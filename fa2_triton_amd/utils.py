@@ -45,8 +45,9 @@ def infer_bias_strides(
 
 def dropout_mask_words(batch: int, heads_q: int, seqlen_q: int, seqlen_k: int) -> int:
     """int32 words of a dropout keep mask (fa2_dropout_mask_bytes / 4 in include/fa2_amd.h):
-    32 x 32 bit tiles, batch * heads_q * ceil(Sq / 32) * ceil(Sk / 32) * 32 words."""
-    return batch * heads_q * ((seqlen_q + 31) // 32) * ((seqlen_k + 31) // 32) * 32
+    32 x 32 bit tiles, batch * heads_q * ceil(Sq / 32) * ceil(Sk / 32) * 32 words, plus one tile of
+    slack (ABI 8: the hand-placed dK/dV reads two key tiles as one run)."""
+    return batch * heads_q * ((seqlen_q + 31) // 32) * ((seqlen_k + 31) // 32) * 32 + 32
 
 
 def check_dropout_mask(mask: torch.Tensor, batch: int, heads_q: int, seqlen_q: int, seqlen_k: int, device) -> None:

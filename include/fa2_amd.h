@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 7
+#define FA2_ABI_VERSION 8
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -70,7 +70,8 @@ typedef struct fa2_fwd_args {
   uint64_t dropout_seed;  /* Philox4x32-10 key, identical to Triton's tl.rand */
   /* optional dropout keep mask out (ABI 6): when non-NULL and dropout_p > 0, the forward also
    * writes the keep bits it drew (keep = tl.rand > p) into this buffer of
-   * fa2_dropout_mask_bytes(batch, heads_q, seqlen_q, seqlen_k) bytes, so that the backward reads
+   * fa2_dropout_mask_bytes(batch, heads_q, seqlen_q, seqlen_k) bytes (ABI 8: the tiles below plus
+   * one 128-byte tile of slack the backward may read past the last one), so that the backward reads
    * them instead of regenerating Philox (fa2_bwd_args.dropout_mask).  Layout: 32 x 32 bit tiles,
    * word[((b * Hq + h) * ceil(Sq / 32) + i / 32) * ceil(Sk / 32) + j / 32][i % 32], bit j % 32 =
    * keep(b, h, i, j).  Only the tiles the (causal) mask leaves visible are written. */

@@ -76,3 +76,21 @@ def run_case(
                           causal=causal, softmax_scale=None, dropout_seed=dropout_seed)
     assert out.shape == q.shape and out.dtype == q.dtype
     return check_fa_tolerance(q, k, v, None if forward_only else do, out, out_ref, out_pt)
+
+
+def assert_dropout_grads_match(got, want, names=("dq", "dk", "dv")):
+    """Gradients of two dropout backwards over the same keep bits.  dQ and dK are bitwise equal
+    whichever kernels ran; dV may come from the hand-placed dK/dV, which packs P M and applies
+    1 / (1 - p) once to the fp32 sum where the general kernel rounds P M / (1 - p) per score
+    (dkdv_hp_kernel.h): within 4 ulps (of the dtype) of the largest |dV|."""
+    for name, x, y in zip(names, got, want):
+        if x is None:
+            continue
+        assert torch.isfinite(x).all(), name
+        if name != "dv":
+            assert torch.equal(x, y), f"{name}: max |diff| {(x.float() - y.float()).abs().max().item():.3e}"
+            continue
+        ulp = 2.0 ** -7 if x.dtype == torch.bfloat16 else 2.0 ** -10
+        tol = 4 * ulp * y.float().abs().max().item()
+        err = (x.float() - y.float()).abs().max().item()
+        assert err <= tol, f"dv: max |diff| {err:.3e} > {tol:.3e}"

@@ -16,7 +16,7 @@ persistent multi-unit paths.
 import pytest
 import torch
 
-from tests.core import generate_attention_mask, generate_test_data
+from tests.core import assert_dropout_grads_match, generate_attention_mask, generate_test_data
 
 BWD_CASES = [
     # b, hq, hkv, sq, sk, causal, dtype
@@ -116,7 +116,8 @@ def test_persistent_units_bitwise_equal_any_grid(b, hq, hkv, s, causal, dtype, v
 @pytest.mark.parametrize("causal", [True, False])
 def test_dropout_hand_placed_dq_multi_unit(causal, cap, policy):
     """The hand-placed dropout dQ reads the forward's saved keep words; several units per workgroup
-    (cap 2) must give the dQ of the general kernel regenerating the keep bits with Philox."""
+    (cap 2) must give the dQ of the general kernel regenerating the keep bits with Philox (dK / dV
+    from the hand-placed dK/dV: assert_dropout_grads_match)."""
     from fa2_triton_amd.backward import _flash_attn_backward
     from fa2_triton_amd.forward import _flash_attn_forward
     from fa2_triton_amd.utils import dropout_mask_words
@@ -130,6 +131,36 @@ def test_dropout_hand_placed_dq_multi_unit(causal, cap, policy):
     policy.set_path_policy(policy.PATH_DQ_HP | policy.PATH_DKDV_HP, 0)
     regen = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=None)
     policy.set_path_policy(0, 0)
-    for name, a, c in zip(("dq", "dk", "dv"), hp[:3], regen[:3]):
-        assert torch.isfinite(a).all(), name
-        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+    assert_dropout_grads_match(hp[:3], regen[:3])
+
+
+DROP_CASES = [
+    # b, hq, hkv, s_q, s_k, causal, p, dtype
+    (2, 4, 2, 1024, 1024, True, 0.1, torch.bfloat16),
+    (2, 4, 4, 1024, 1024, False, 0.2, torch.float16),
+    (1, 8, 2, 777, 333, True, 0.17, torch.bfloat16),
+    (1, 2, 1, 300, 700, False, 0.3, torch.bfloat16),
+    (2, 2, 2, 129, 257, True, 0.1, torch.float16),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,p,dtype", DROP_CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_dropout_hand_placed_dkdv(b, hq, hkv, sq, sk, causal, p, dtype, cap, policy):
+    """The hand-placed dK/dV with the forward's saved keep words (ABI 8) against the general
+    dK/dV over the same words: dK bitwise (dS = P (dP kp - delta) in the same operations), dV as
+    assert_dropout_grads_match; one and several blocks per workgroup (cap 3), ragged and GQA."""
+    from fa2_triton_amd.backward import _flash_attn_backward
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from fa2_triton_amd.utils import dropout_mask_words
+
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, 128, dtype)
+    words = torch.empty(dropout_mask_words(b, hq, sq, sk), dtype=torch.int32, device="cuda")
+    o, lse, scale, seed = _flash_attn_forward(q, k, v, None, None, p, causal, None, 4321, dropout_mask=words)
+    policy.set_path_policy(0, cap)
+    hp = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=words)
+    policy.set_path_policy(policy.PATH_DKDV_HP, 0)
+    gen = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=words)
+    policy.set_path_policy(0, 0)
+    assert_dropout_grads_match(hp[:3], gen[:3])
