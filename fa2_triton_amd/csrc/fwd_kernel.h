@@ -402,7 +402,8 @@ hipError_t launch_fwd_dt(const fa2_fwd_args& a, bool aligned, hipStream_t st) {
   // are 16-byte aligned (its tiles are staged by LDS-DMA)
   if constexpr (DT == 128) {
     // hand-placed one-wave-per-SIMD kernel (fwd_hp_kernel.h) for D = 128 exactly
-    if (fwd_hp_ok(a, aligned)) return c ? launch_fwd_hp<BF16, true>(a, st) : launch_fwd_hp<BF16, false>(a, st);
+    if (a.head_dim == DT && fwd_hp_ok(a, aligned))
+      return c ? launch_fwd_hp<BF16, true, DT>(a, st) : launch_fwd_hp<BF16, false, DT>(a, st);
   }
   if constexpr (DT == 64 || DT == 128) {
     const bool bias16 = bias16_rows(a.bias, a.bias_dtype, a.bias_stride);

@@ -374,11 +374,20 @@ class FwdGen:
     with -m_ref, so the chain yields z directly (no per-score VALU; costs one extra rounding of
     the scores, ~2^-9 relative in bf16)."""
 
-    def __init__(self, bf16, causal, exact=True, stamp=False):
+    def __init__(self, bf16, causal, exact=True, stamp=False, dt=128):
         self.bf16, self.causal, self.exact, self.stamp = bf16, causal, exact, stamp
+        # head dim: 128 (8 k-steps, 4 d-tiles) or 64 (4, 2); a 64-row K / V tile is dt / 8 KiB,
+        # staged in dt / 32 LDS-DMA pieces of 4 KiB
+        self.dt, self.ks, self.ndt, self.np = dt, dt // 16, dt // 32, dt // 32
+        self.tile = 64 * dt * 2
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
+
+    def o(self, rb, dt, i=None):
+        """O^T accumulators of (row block, d-tile): a[0 : 32 ndt]."""
+        base = (rb * self.ndt + dt) * 16
+        return rng("a", base, 16) if i is None else f"a{base + i}"
 
     def chain0(self, rb):
         """Initial accumulator of an S chain: 0 (exact) or INIT = -m_ref (pre-scaled Q)."""
@@ -386,17 +395,17 @@ class FwdGen:
 
     # -- pieces ------------------------------------------------------------------------------
     def k_read(self, kbuf, m):
-        """K fragment m (key half t = m // 8, k-step ks = m % 8) of the buffer kbuf -> ring."""
-        t, ks = m // 8, m % 8
-        imm = kbuf * 16384 + (ks >> 1) * 4096 + 32 * t * 64
+        """K fragment m (key half t = m // ks, k-step m % ks) of the buffer kbuf -> ring."""
+        t, ks = m // self.ks, m % self.ks
+        imm = kbuf * self.tile + (ks >> 1) * 4096 + 32 * t * 64
         base = "%[kb1]" if ks & 1 else "%[kb0]"
         dst = KR(m % 4)
         self.e.ds_read(f"ds_read_b128 {dst}, {base} offset:{imm}", dst)
 
     def v_read(self, vbuf, m, half):
-        """Half `half` of V^T fragment m (kk = m // 4, dt = m % 4) of V buffer vbuf -> ring."""
-        kk, dt = m // 4, m % 4
-        imm = 32768 + vbuf * 16384 + dt * 4096 + 16 * kk * 64
+        """Half `half` of V^T fragment m (kk = m // ndt, dt = m % ndt) of V buffer vbuf -> ring."""
+        kk, dt = m // self.ndt, m % self.ndt
+        imm = 2 * self.tile + vbuf * self.tile + dt * 4096 + 16 * kk * 64
         base = "%[vb]" if half else "%[va]"
         dst = VR(m % 4, half)
         self.e.ds_read(f"ds_read_b64_tr_b16 {dst}, {base} offset:{imm}", dst)
@@ -404,10 +413,10 @@ class FwdGen:
     def dma_piece(self, which, par, it):
         """LDS-DMA piece `it` of this wave: K(i+2) into K buffer par, V(i+1) into V buffer 1-par."""
         if which == "k":
-            imm = par * 16384 + it * 4096
+            imm = par * self.tile + it * 4096
             desc = SKD
         else:
-            imm = 32768 + (1 - par) * 16384 + it * 4096
+            imm = 2 * self.tile + (1 - par) * self.tile + it * 4096
             desc = SVD
         self.e.salu(f"s_add_u32 m0, %[mlds], {imm}", m0=True)
         self.e.dma(f"buffer_load_dwordx4 %[off{it}], {desc}, 0 offen lds")
@@ -513,7 +522,7 @@ class FwdGen:
                 for c in range(2):
                     e.valu(f"v_mul_f32 {LSUM[rb][c]}, {t_alpha}, {LSUM[rb][c]}", LSUM[rb][c], [t_alpha, LSUM[rb][c]])
             # O[rb] *= alpha, in groups of len(scratch)
-            regs = [] if first else [O(rb, dt, i) for dt in range(4) for i in range(16)]
+            regs = [] if first else [self.o(rb, dt, i) for dt in range(self.ndt) for i in range(16)]
             g = len(scratch)
             for k in range(0, len(regs), g):
                 grp = regs[k:k + g]
@@ -569,15 +578,16 @@ class FwdGen:
         """S(0) = K(0) Q^T (+ INIT) into set st (K(0) in K buffer st), fragments read LEADK ahead;
         no fillers."""
         e = self.e
+        nk = 2 * self.ks
         for m in range(LEADK):
             self.k_read(st, m)
-        for m in range(16):
-            if m + LEADK < 16:
+        for m in range(nk):
+            if m + LEADK < nk:
                 self.k_read(st, m + LEADK)
-            t, ks = m // 8, m % 8
+            t, ks = m // self.ks, m % self.ks
             for rb in range(2):
                 d = S(st, rb, t)
-                e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", self.chain0(rb) if ks == 0 else d)
+                e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * self.ks + ks}]", self.chain0(rb) if ks == 0 else d)
 
     def max_mask_plain(self, st, masked):
         """Mask (masked tiles) and row max of set st, no MFMA cover (prologue)."""
@@ -605,7 +615,7 @@ class FwdGen:
         if final:
             # the next unit's loads stay in flight across the epilogue (its statement waits)
             e.drain_lds()
-            e.raw(f"s_waitcnt vmcnt({N_NEXT})")
+            e.raw(f"s_waitcnt vmcnt({3 * self.np + 2 * self.ks})")
             e.raw("s_barrier")
             e.reset()
         else:
@@ -620,9 +630,9 @@ class FwdGen:
         pieces = [(1 - par, "k0"), (1 - par, "v0"), (par, "k1")]
 
         def lds_of(buf, what, it):
-            return (32768 if what == "v0" else 0) + buf * 16384 + it * 4096
+            return (2 * self.tile if what == "v0" else 0) + buf * self.tile + it * 4096
 
-        seq = [(buf, what, it) for buf, what in pieces for it in range(4)]
+        seq = [(buf, what, it) for buf, what in pieces for it in range(self.np)]
         out = []
 
         def desc(what):
@@ -644,7 +654,7 @@ class FwdGen:
             def f(n=n, buf=buf, what=what, it=it):
                 if n == 0:
                     e.salu(f"s_add_u32 m0, %[mlds], {lds_of(buf, what, it)}", m0=True)
-                if n == 8:  # tile 1 of K: one tile further, range one tile shorter
+                if n == 2 * self.np:  # tile 1 of K: one tile further, range one tile shorter
                     e.salu("s_add_u32 s68, s68, %[tileb]")
                     e.salu("s_addc_u32 s69, s69, 0")
                     e.salu("s_sub_i32 s70, s70, %[tileb]")
@@ -661,9 +671,9 @@ class FwdGen:
             e.salu("s_mov_b32 s75, 0x20000")
         out.append((8, qdesc))
         for rb in range(2):
-            for ks in range(8):
+            for ks in range(self.ks):
                 def f(rb=rb, ks=ks):
-                    e.raw(f"buffer_load_dwordx4 %[q{rb * 8 + ks}], %[nqo{rb}], s[72:75], 0 offen offset:{32 * ks}")
+                    e.raw(f"buffer_load_dwordx4 %[q{rb * self.ks + ks}], %[nqo{rb}], s[72:75], 0 offen offset:{32 * ks}")
                 out.append((16, f))
         return out
 
@@ -687,65 +697,91 @@ class FwdGen:
             for rb in range(2):
                 e.valu(f"v_subrev_u32 {REL[rb]}, {SN1}, %[rel{rb}]", REL[rb], [])
         # ---------------- phase X ----------------
-        n_x_exp = 56 if qk else 64
-        gx = GapScheduler(32 if qk else 0)
+        nk = 2 * self.ks        # K fragments per tile (two MFMAs each)
+        nx = 2 * nk             # phase X MFMAs (32 at D = 128)
+        # exponentials of tile i in phase X: all but (part of) the last 16-key group, whose packs
+        # come last in phase Y (D = 64: 48, the kk = 3 group in Y)
+        n_x_exp = (56 if self.dt == 128 else 48) if qk else 64
+        gx = GapScheduler(nx if qk else 0)
         if qk:
-            for m in range(16):
-                if m + LEADK < 16:
+            for m in range(nk):
+                if m + LEADK < nk:
                     gx.add("k", 4, 2 * m, 2 * m, lambda m=m: self.k_read(kbuf, m + LEADK))
+        x_dl = [(n * (nx - 2)) // n_x_exp for n in range(n_x_exp)]
         for n, el in enumerate(E[:n_x_exp]):
-            gx.add("exp", 8, -1, (n * 30) // n_x_exp, lambda el=el: self.exp(cur, el))
+            gx.add("exp", 8, -1, x_dl[n], lambda el=el: self.exp(cur, el))
         for n, f in enumerate(dma):
-            gx.add("dma", f[0], -1, min(31, 4 * n + 3), f[1])
+            gx.add("dma", f[0], -1, min(nx - 1, (4 * n + 3) * nx // 32), f[1])
+        # a pack reads the exponentials of E[16 kk + 8 rb + 2 j], + 1 (elem_order); D = 64 orders
+        # it after them explicitly (streams order only themselves: with a crowded gap a cheaper
+        # item could otherwise run ahead of an exponential of another stream)
+        order = self.dt == 64
+
+        def after(idx, dls):
+            return max(dls[i] for i in idx) + 1 if order else -1
         cv = [(rb, kk, j) for kk in range(4 if not qk else 1) for rb in range(2) for j in range(4)]
         for n, c in enumerate(cv):
-            gx.add("cvt", 4, -1, 31, lambda c=c: self.cvt(cur, *c))
+            rb_, kk_, j_ = c
+            idx = [16 * kk_ + 8 * rb_ + 2 * j_, 16 * kk_ + 8 * rb_ + 2 * j_ + 1]
+            gx.add("cvt", 4, min(nx - 1, after(idx, x_dl)), nx - 1, lambda c=c: self.cvt(cur, *c))
         for m in range(LEADV):
             for h in range(2):
-                gx.add("vr", 4, 20, 31, lambda m=m, h=h: self.v_read(vbuf, m, h))
+                gx.add("vr", 4, max(0, nx - 12), nx - 1, lambda m=m, h=h: self.v_read(vbuf, m, h))
 
         def x_mfma(g):
             m, rb = g >> 1, g & 1
-            t, ks = m // 8, m % 8
+            t, ks = m // self.ks, m % self.ks
             d = S(nxt, rb, t)
-            e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * 8 + ks}]", self.chain0(rb) if ks == 0 else d)
+            e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * self.ks + ks}]", self.chain0(rb) if ks == 0 else d)
 
         if qk:
             for m in range(LEADK):
                 self.k_read(kbuf, m)
         gx.run(x_mfma, pre_budget=40)
         # ---------------- phase Y ----------------
-        gy = GapScheduler(32)
-        for m in range(16):
-            if m + LEADV < 16:
+        nv = 4 * self.ndt       # V^T fragments per tile (two MFMAs each)
+        ny = 2 * nv             # phase Y MFMAs (32 at D = 128)
+        gy = GapScheduler(ny)
+        for m in range(nv):
+            if m + LEADV < nv:
                 for h in range(2):
                     gy.add("v", 4, 2 * m, 2 * m + 1, lambda m=m, h=h: self.v_read(vbuf, m + LEADV, h))
+        n_y_exp = len(E) - n_x_exp
+        y_dl = {}  # element index -> deadline of its exponential in phase Y
         for n, el in enumerate(E[n_x_exp:]):
-            gy.add("exp", 8, -1, 4 + n, lambda el=el: self.exp(cur, el))
+            dl = 4 + n if self.dt == 128 else 2 + (n * 6) // max(1, n_y_exp)
+            y_dl[n_x_exp + n] = dl
+            gy.add("exp", 8, -1, dl, lambda el=el: self.exp(cur, el))
+
+        def after_y(idx):
+            return max([y_dl[i] for i in idx if i in y_dl] + [-2]) + 1 if order else -1
         if qk:
-            for kk, dl in ((1, 5), (2, 13), (3, 21)):
+            # packs of P(kk) before the first PV MFMA reading them (MFMA 2 ndt kk)
+            for kk in (1, 2, 3):
+                dl = (5, 13, 21)[kk - 1] if self.dt == 128 else 2 * self.ndt * kk - 3
                 for rb in range(2):
                     for j in range(4):
-                        gy.add(f"cvt{kk}", 4, -1, dl, lambda c=(rb, kk, j): self.cvt(cur, *c))
+                        idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
+                        gy.add(f"cvt{kk}", 4, after_y(idx), dl, lambda c=(rb, kk, j): self.cvt(cur, *c))
             for t in range(2):
                 for rb in range(2):
                     if masked:
                         for i in range(16):
-                            gy.add(f"mx{t}{rb}", 8, 16 * t - 1, 31,
+                            gy.add(f"mx{t}{rb}", 8, (ny // 2) * t - 1, ny - 1,
                                    lambda rb=rb, t=t, i=i: self.mask_elem(nxt, rb, t, i))
                     for op in self.max_ops_z(nxt, rb, t):
                         if op[0] == "max":
-                            gy.add(f"mx{t}{rb}", 4, 16 * t - 1, 31,
+                            gy.add(f"mx{t}{rb}", 4, (ny // 2) * t - 1, ny - 1,
                                    lambda op=op: e.valu(op[1], op[2], op[3]))
                         else:
-                            gy.add(f"mx{t}{rb}", 4, 16 * t - 1, 31, lambda op=op: self.fma_z(nxt, *op[1:]))
+                            gy.add(f"mx{t}{rb}", 4, (ny // 2) * t - 1, ny - 1, lambda op=op: self.fma_z(nxt, *op[1:]))
         for n, el in enumerate(E):
-            gy.add(f"add{n % 2}", 4, 0, 31, lambda el=el, c=n % 2: self.add(cur, el, c))
+            gy.add(f"add{n % 2}", 4, max(0, after_y([n])), ny - 1, lambda el=el, c=n % 2: self.add(cur, el, c))
 
         def y_mfma(g):
             m, rb = g >> 1, g & 1
-            kk, dt = m >> 2, m & 3
-            e.mfma(self.mop, O(rb, dt), VR(m % 4), PF(rb, kk), O(rb, dt))
+            kk, dt = m // self.ndt, m % self.ndt
+            e.mfma(self.mop, self.o(rb, dt), VR(m % 4), PF(rb, kk), self.o(rb, dt))
 
         gy.run(y_mfma, pre_budget=0)
         if qk:
@@ -756,10 +792,10 @@ class FwdGen:
     def dma_stream(self, par):
         """The period's 8 LDS-DMA pieces as (cost, emit) items; each item issues its piece and
         already points m0 at the next one, so no piece waits on its own m0 write."""
-        pieces = [("k", it) for it in range(4)] + [("v", it) for it in range(4)]
+        pieces = [("k", it) for it in range(self.np)] + [("v", it) for it in range(self.np)]
 
         def m0_of(w_, it):
-            return par * 16384 + it * 4096 if w_ == "k" else 32768 + (1 - par) * 16384 + it * 4096
+            return par * self.tile + it * 4096 if w_ == "k" else 2 * self.tile + (1 - par) * self.tile + it * 4096
 
         out = []
         for n, (w_, it) in enumerate(pieces):
@@ -802,9 +838,9 @@ class FwdGen:
             for j in range(1 if self.exact else 16):
                 e.valu(f"v_mov_b32 {INIT(rb, j)}, 0", INIT(rb, j))
         for rb in range(2):
-            for dt in range(4):
+            for dt in range(self.ndt):
                 for i in range(16):
-                    e.valu(f"v_accvgpr_write_b32 {O(rb, dt, i)}, 0", O(rb, dt, i), kind="accw")
+                    e.valu(f"v_accvgpr_write_b32 {self.o(rb, dt, i)}, 0", self.o(rb, dt, i), kind="accw")
         # DMA cursors: period i requests K(i + 2) and V(i + 1)
         e.salu(f"s_mov_b32 {SKP[0]}, %[klo]")
         e.salu(f"s_mov_b32 {SKP[1]}, %[khi]")
@@ -2128,27 +2164,32 @@ FA2_DEV void dq_hp_load_next(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a) 
 """
 
 
-def gen_fwd_function(bf16, causal, exact=True):
+def gen_fwd_function(bf16, causal, exact=True, dt=128):
     out = []
+    nq = 2 * (dt // 16)  # Q fragments (two row blocks x k-steps)
     for stamp in (False, True):
-        g = FwdGen(bf16, causal, exact, stamp)
+        g = FwdGen(bf16, causal, exact, stamp, dt)
         lines = g.build()
-        name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}"
-        clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in AGPR_CLOBBER] + \
+        name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}" + \
+            ("" if dt == 128 else f"_d{dt}")
+        # O^T a[0 : dt], K / V^T rings a[192:223]; every AGPR but the Q operands' (a[128:191] at
+        # D = 128, a[64:95] at D = 64) clobbered, so the compiler has no room to move them
+        acc = list(range(0, dt)) + list(range(dt + 2 * dt // 4 if dt == 64 else 192, 256))
+        clob = [f'"v{i}"' for i in range(N_VGPR)] + [f'"a{i}"' for i in acc] + \
                [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
-        qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))
+        qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(nq))
         stops = ", " + ", ".join(f'[st{i}] "=&s"(st[{i}])' for i in range(4)) if stamp else ""
         starg = ", uint32_t (&st)[4]" if stamp else ""
         out.append(f"""{'#if FA2_HP_STAMPS' if stamp else '#if !FA2_HP_STAMPS'}
 // hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}{', stamped' if stamp else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 // q: this unit's Q fragments in, the NEXT unit's Q fragments out -- still in flight (the next
 // statement waits for them first; nothing may read q in between)
-FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]{starg}) {{
+FA2_DEV void {name}(u32x4 (&q)[{nq}], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]{starg}) {{
   asm volatile(
 {_asm_body(lines)}
       : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1]), {qops}{stops}
       : [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),
-        [off0] "v"(a.off[0]), [off1] "v"(a.off[1]), [off2] "v"(a.off[2]), [off3] "v"(a.off[3]),
+        {", ".join(f'[off{i}] "v"(a.off[{i}])' for i in range(dt // 32))},
         [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]), [nqo0] "v"(a.nqo[0]), [nqo1] "v"(a.nqo[1]),
         [na] "s"(a.na), [last] "s"(a.last), [ntiles] "s"(a.ntiles), [mask0] "s"(a.mask0),
         [tileb] "s"(a.tileb), [kbytes] "s"(a.kbytes), [mlds] "s"(a.mlds),
@@ -2169,15 +2210,17 @@ FA2_DEV void {name}(u32x4 (&q)[16], const FwdHpArgs& a, float (&m_out)[2], float
 ACC_CLOBBER = ", ".join(f'"a{i}"' for i in range(128))
 
 
-def gen_read_o():
-    parts = ["// O^T accumulators a[0:127] -> registers (after the main statement's final drain)",
-             "FA2_DEV void fwd_hp_read_o(f32x16 (&o)[2][4]) {"]
+def gen_read_o(ndt=4):
+    n = 32 * ndt
+    clob = ", ".join(f'"a{i}"' for i in range(n))
+    parts = [f"// O^T accumulators a[0:{n - 1}] -> registers (after the main statement's final drain)",
+             f"FA2_DEV void fwd_hp_read_o{'' if ndt == 4 else f'_d{32 * ndt}'}(f32x16 (&o)[2][{ndt}]) {{"]
     for rb in range(2):
-        for dt in range(4):
-            base = (rb * 4 + dt) * 16
+        for dt in range(ndt):
+            base = (rb * ndt + dt) * 16
             outs = ", ".join(f'"=v"(o[{rb}][{dt}][{i}])' for i in range(16))
             body = "".join(f"v_accvgpr_read_b32 %{i}, a{base + i}\\n" for i in range(16))
-            parts.append(f'  asm volatile("{body}" : {outs} : : {ACC_CLOBBER});')
+            parts.append(f'  asm volatile("{body}" : {outs} : : {clob});')
     parts.append("}")
     return "\n".join(parts) + "\n"
 
@@ -2189,6 +2232,8 @@ def write_headers():
         for causal in (True, False):
             for exact in (True, False):
                 out.append(gen_fwd_function(bf16, causal, exact))
+            # (FwdGen(dt=64) builds a D = 64 unit too; measured no faster than fwd_pipe_kernel at
+            # D = 64, where the softmax VALU bounds both -- DESIGN.md section 6 -- so not emitted)
     out.append(gen_read_o())
     out.append("}  // namespace fa2\n")
     text = "\n".join(out)

@@ -119,7 +119,7 @@ def test_every_kernel_fits_the_cu(kernels):
 
 # the hand-placed one-wave-per-SIMD kernels (hp_gen.py): whole register file, zero scratch
 HP = {
-    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb1EEEv12fa2_fwd_args",
+    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb1ELi128EEEv12fa2_fwd_args",
     "dkdv_hp": r"_ZN3fa214dkdv_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_bwd_argsi",
     "dq_hp": r"_ZN3fa212dq_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_bwd_args",
 }
@@ -158,7 +158,7 @@ def _disassemble(co: bytes, tmp_path, n):
 def test_accumulators_untouched_until_read(tmp_path, kind):
     if not os.path.exists(_lib.LIB_PATH) or not os.path.exists(OBJDUMP):
         pytest.skip("library or llvm-objdump missing")
-    n_acc = ACC_RANGE[kind]
+    n_acc0 = ACC_RANGE[kind]
     sym = {"fwd_hp": "fwd_hp_kernel", "dq_hp": "dq_hp_kernel", "dkdv_hp": "dkdv_hp_kernel"}[kind]
     checked = 0
     for n, co in enumerate(_code_objects(_lib.LIB_PATH)):
@@ -168,6 +168,7 @@ def test_accumulators_untouched_until_read(tmp_path, kind):
         for func in re.split(r"\n(?=[0-9a-f]+ <)", text):
             if sym not in func.split("\n", 1)[0]:
                 continue
+            n_acc = n_acc0
             lines = [ln.split("//")[0].strip() for ln in func.split("\n")[1:]]
             lines = [ln for ln in lines if ln]
             i = 0
