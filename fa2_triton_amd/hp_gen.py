@@ -1100,19 +1100,25 @@ D_G = "s64"        # q-head index in the group
 D_IDX = "s65"      # step index within the head
 D_CM = "s66"       # first query row of the current tile
 D_PAR = "s67"      # step phase i mod DK_NBUF (buffer of step i; S set = phase & 1)
-D_QD = "s[68:71]"  # descriptors of the requested step's Q, dO, LSE2 and delta rows
+# descriptors of the requested step's Q, dO, LSE2 and delta rows; their base words ARE the
+# cursors (the requested tile's first byte; stride 0, and a 48-bit address leaves the high
+# word's stride bits clear), word 2 the range of the step, word 3 constant
+D_QD = "s[68:71]"
 D_OD = "s[72:75]"
 D_LD = "s[76:79]"
 D_DD = "s[80:83]"
-D_QP = ("s84", "s85")  # requested step's Q tile address, dO tile address
-D_OP = ("s86", "s87")
-D_LC = "s88"       # requested step's LSE2 / delta byte offset from the row bases
+D_QP = ("s68", "s69")
+D_OP = ("s72", "s73")
+D_LP = ("s76", "s77")
+D_DP = ("s80", "s81")
+D_MD = "s[84:87]"  # dropout: keep-word descriptor (constant through the statement)
+D_WL = "s88"       # dropout: LDS base of this wave's keep words in buffer 0
 D_NM = "s89"       # requested step's first query row
 D_LEFT = "s90"     # total steps - the requested step's index (> 0: it exists)
 D_NMT = "s91"      # requested step's tile index within its head
 D_M0 = "s92"
 D_T = "s93"
-D_EX = "s[94:95]"  # exec save of the rows DMA; s94 also the rows' range (descriptor items 0 -> 2)
+D_EX = "s[94:95]"  # exec save of the rows DMA
 D_MK = ["s[96:97]", "s[98:99]"]
 
 
@@ -1126,6 +1132,8 @@ class DkdvGen:
     def __init__(self, bf16, causal, dropout=False):
         self.bf16, self.causal, self.dropout = bf16, causal, dropout
         assert not (dropout and DVF_SLOTS != 4), "the dropout -delta rows use the V ring's 4 slots"
+        self.vslots = DVF_SLOTS
+        self.nvgpr = DK_NVGPR_DROP if dropout else DK_NVGPR
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
@@ -1143,7 +1151,7 @@ class DkdvGen:
         ks, kb = n >> 1, n & 1
         imm = (ks >> 1) * 4096 + 32 * kb * 64
         base = "%[vb1]" if ks & 1 else "%[vb0]"
-        d = DVF(n)
+        d = self.dvf(n)
         self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
 
     def tr_read(self, buf, dout, f, half, dst):
@@ -1154,6 +1162,9 @@ class DkdvGen:
         base = "%[tb]" if half else "%[ta]"
         self.e.ds_read(f"ds_read_b64_tr_b16 {dst}, {base} offset:{imm}", dst)
 
+    def dvf(self, n):
+        return rng("v", 128 + 4 * (n % self.vslots), 4)
+
     def init_read(self, buf, what, kb, g4):
         """LSE2 (what 0; g4 in the half's pair) rows into the LSE registers, -delta (what 1) into
         dP[kb] (the dP chain's initial accumulator): register group g4."""
@@ -1162,35 +1173,24 @@ class DkdvGen:
         self.e.ds_read(f"ds_read_b128 {d}, %[lb] offset:{imm}", d)
 
     def descriptors(self, part=None):
-        """Descriptors of the requested step's tiles from the cursors (range 0 when none); part
-        0: the ranges (D_T rows, s94 the rows' bytes), 1: Q and dO, 2: LSE2 and delta rows."""
+        """The ranges of the requested step's descriptors (range 0 when none): part 0 the rows
+        (D_T) and the LSE2 / delta bytes below Lq, 1 the Q and dO bytes."""
         e = self.e
-        t2 = "s94"  # (D_EX, free outside the rows' DMA)
         if part in (None, 0):
             e.salu(f"s_sub_u32 {D_T}, %[lq], {D_NM}")
             e.salu(f"s_cmp_gt_i32 {D_LEFT}, 0")
             e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
-            # LSE2 / delta bytes of the rows below Lq (rows past it read as zeros)
-            e.salu(f"s_min_u32 {t2}, {D_T}, 32")
-            e.salu(f"s_lshl_b32 {t2}, {t2}, 2")
+            e.salu(f"s_min_u32 s78, {D_T}, 32")
+            e.salu("s_lshl_b32 s78, s78, 2")
             if self.dropout:  # lsoff = sb + DK_W0 + 256 w + 4 lane (w = 0 here): the range
                 # starts there (lbs = sb + DK_ROWS)
-                e.salu(f"s_add_u32 {t2}, {t2}, %[lbs]")
-                e.salu(f"s_add_u32 {t2}, {t2}, {DK_W0 - DK_ROWS}")
+                e.salu("s_add_u32 s78, s78, %[lbs]")
+                e.salu(f"s_add_u32 s78, s78, {DK_W0 - DK_ROWS}")
+            e.salu("s_mov_b32 s82, s78")
         if part in (None, 1):
             orb = "%[qrb]" if self.dropout else "%[orb]"  # (dropout: one row stride)
-            for (p0, p1), rb, d in ((D_QP, "%[qrb]", 68), (D_OP, orb, 72)):
-                e.salu(f"s_mov_b32 s{d}, {p0}")
-                e.salu(f"s_and_b32 s{d + 1}, {p1}, 0xffff")
-                e.salu(f"s_mul_i32 s{d + 2}, {D_T}, {rb}")
-                e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
-        if part in (None, 2):
-            for base, d in (("lse", 76), ("dl", 80)):
-                e.salu(f"s_add_u32 s{d}, %[{base}lo], {D_LC}")
-                e.salu(f"s_addc_u32 s{d + 1}, %[{base}hi], 0")
-                e.salu(f"s_and_b32 s{d + 1}, s{d + 1}, 0xffff")
-                e.salu(f"s_mov_b32 s{d + 2}, {t2}")
-                e.salu(f"s_mov_b32 s{d + 3}, 0x20000")
+            e.salu(f"s_mul_i32 s70, {D_T}, %[qrb]")
+            e.salu(f"s_mul_i32 s74, {D_T}, {orb}")
 
     def advance_cursors(self, tag):
         """Cursors to the step after the requested one: one tile down, or the next head's last
@@ -1208,7 +1208,9 @@ class DkdvGen:
         e.salu(f"s_lshl_b32 {D_T}, {'%[qrb]' if self.dropout else '%[orb]'}, 5")
         e.salu(f"s_sub_u32 {D_OP[0]}, {D_OP[0]}, {D_T}")
         e.salu(f"s_subb_u32 {D_OP[1]}, {D_OP[1]}, 0")
-        e.salu(f"s_sub_u32 {D_LC}, {D_LC}, 128")
+        for p0, p1 in (D_LP, D_DP):
+            e.salu(f"s_sub_u32 {p0}, {p0}, 128")
+            e.salu(f"s_subb_u32 {p1}, {p1}, 0")
         if self.dropout:
             e.salu(f"s_sub_u32 {D_MC}, {D_MC}, %[mstep]")
         e.raw(f"s_branch .Lhp%=_{tag}_adv")
@@ -1219,7 +1221,9 @@ class DkdvGen:
         e.salu(f"s_addc_u32 {D_QP[1]}, {D_QP[1]}, 0")
         e.salu(f"s_add_u32 {D_OP[0]}, {D_OP[0]}, %[owrap]")
         e.salu(f"s_addc_u32 {D_OP[1]}, {D_OP[1]}, 0")
-        e.salu(f"s_add_u32 {D_LC}, {D_LC}, %[lwrap]")
+        for p0, p1 in (D_LP, D_DP):
+            e.salu(f"s_add_u32 {p0}, {p0}, %[lwrap]")
+            e.salu(f"s_addc_u32 {p1}, {p1}, 0")
         if self.dropout:
             e.salu(f"s_add_u32 {D_MC}, {D_MC}, %[mwrap]")
         e.label(f".Lhp%=_{tag}_adv")
@@ -1234,7 +1238,7 @@ class DkdvGen:
             return nb * 16384 + (8192 if w_ == "o" else 0) + it * 4096
 
         # (issue costs of scalar instructions are taken as 2 cycles each)
-        out = [(8, lambda: self.descriptors(0)), (16, lambda: self.descriptors(1)), (20, lambda: self.descriptors(2))]
+        out = [(12, lambda: self.descriptors(0)), (4, lambda: self.descriptors(1))]
 
         def rows(tag=tag):
             e = self.e
@@ -1254,18 +1258,11 @@ class DkdvGen:
         if self.dropout:
             def words(nb=nb):
                 # this wave's 64 keep words of the requested step (rows of the tile, key tiles
-                # kt0, kt0 + 1: one word per lane); D_LD is free again after the rows
+                # kt0, kt0 + 1: one word per lane)
                 e = self.e
-                e.salu("s_mov_b32 s76, %[mlo]")
-                e.salu("s_mov_b32 s77, %[mhi]")
-                e.salu("s_mov_b32 s79, 0x20000")
-                # m0 = sb + DK_W0 + 1024 nb + 256 w
-                e.salu("s_lshl_b32 s78, %[w0], 8")
-                e.salu(f"s_add_u32 s78, s78, %[lbs]")
-                e.salu(f"s_add_u32 m0, s78, {DK_W0 - DK_ROWS + nb * 1024}", m0=True)
-                e.salu("s_mov_b32 s78, -1")
-                e.dma(f"buffer_load_dword %[lsoff], s[76:79], {D_MC} offen lds")
-            out.append((16, words))
+                e.salu(f"s_add_u32 m0, {D_WL}, {nb * 1024}", m0=True)
+                e.dma(f"buffer_load_dword %[lsoff], {D_MD}, {D_MC} offen lds")
+            out.append((8, words))
         for n, (w_, it) in enumerate(pieces):
             def f(n=n, w_=w_, it=it):
                 if n == 0:
@@ -1344,13 +1341,16 @@ class DkdvGen:
         e = self.e
         o = (i & 3) + 8 * (i >> 2)
         r = DS(st, kb, i)
-        # s98: not s94, which carries the rows' range from one descriptor item to the next
-        e.salu(f"s_add_u32 s98, {D_CM}, {o}")
-        e.salu(f"s_sub_u32 s98, s98, %[kd0]")
-        if kb:
-            e.salu("s_sub_u32 s98, s98, 32")
-        e.valu(f"v_cmp_ge_i32_e64 {D_MK[0]}, s98, %[lr]", None, [])
-        e.valu(f"v_cndmask_b32_e64 {r}, 0, {r}, {D_MK[0]}", r, [r])
+        # s96 + kb = CM - kd[kb] (mask_bases, at the step start)
+        e.salu(f"s_add_u32 s98, s{96 + kb}, {o}")
+        e.valu("v_cmp_ge_i32_e32 vcc, s98, %[lr]", None, [])
+        e.valu(f"v_cndmask_b32_e32 {r}, 0, {r}, vcc", r, [r])
+
+    def mask_bases(self):
+        """s96 + kb = CM - kd[kb] of a masked step (kd[1] = kd[0] + 32)."""
+        e = self.e
+        e.salu(f"s_sub_u32 s96, {D_CM}, %[kd0]")
+        e.salu("s_sub_u32 s97, s96, 32")
 
     def cvt(self, d, a, b):
         self.e.valu(f"{self.cvtop} {d}, {a}, {b}", d, [a, b])
@@ -1376,6 +1376,8 @@ class DkdvGen:
         nxt = (par + 1) % DK_NBUF
         live = cls in ("A", "B")
         masked = cls == "B"
+        if masked and self.causal:
+            self.mask_bases()
         g = GapScheduler(64 if live else 24, lds_cap=None if "dk_nocap" in ABL else 3)
         # Q(i+1) row fragments ks -> ring slot ks % 4 (after the slot's previous occupant's last
         # MFMA: the straddled MFMAs 2 dt + kb, then S MFMAs 8 + 2 ks + kb)
@@ -1397,7 +1399,7 @@ class DkdvGen:
                           lambda dt=dt, h=h: self.tr_read(par, False, 4 + dt, h, DRR(dt, h)), lds=1)
             # V fragments n (slot n % 4): dP MFMA 24 + n
             for n in range(16):
-                rel = 8 if n < DVF_SLOTS else 24 + n - DVF_SLOTS
+                rel = 8 if n < self.vslots else 24 + n - self.vslots
                 g.add("vf", 4, rel, max(rel, 21 + n), lambda n=n: self.v_frag(n), lds=2)
             # dO^T fragments f (slot f % 4): dV MFMAs 40 + 2 f + kb; then Q^T rows 0-15 (slot f)
             for f in range(8):
@@ -1520,7 +1522,7 @@ class DkdvGen:
             elif m < 40:  # dP[kb] += dO(ks) V[kb](ks), both chains seeded from dP[1]'s -delta rows
                 ks, kb = (m - 24) >> 1, m & 1
                 c = ("0" if self.dropout else DDP(1)) if ks == 0 else DDP(kb)
-                e.mfma(self.mop, DDP(kb), DRR(ks), DVF(2 * ks + kb), c)
+                e.mfma(self.mop, DDP(kb), DRR(ks), self.dvf(2 * ks + kb), c)
             elif m < 56:  # dV^T[kb][dt] += dO^T(sp, dt) P[kb](sp)
                 f, kb = (m - 40) >> 1, m & 1
                 e.mfma(self.mop, DDV(kb, f & 3), DTR(f), DPP(kb, f >> 2), DDV(kb, f & 3))
@@ -1560,7 +1562,20 @@ class DkdvGen:
         e.salu(f"s_mov_b32 {D_QP[1]}, %[qhi]")
         e.salu(f"s_mov_b32 {D_OP[0]}, %[olo]")
         e.salu(f"s_mov_b32 {D_OP[1]}, %[ohi]")
-        e.salu(f"s_mov_b32 {D_LC}, %[lc0]")
+        for (p0, p1), b in ((D_LP, "lse"), (D_DP, "dl")):
+            e.salu(f"s_add_u32 {p0}, %[{b}lo], %[lc0]")
+            e.salu(f"s_addc_u32 {p1}, %[{b}hi], 0")
+        for d in (71, 75, 79, 83):
+            e.salu(f"s_mov_b32 s{d}, 0x20000")
+        if self.dropout:
+            e.salu("s_mov_b32 s84, %[mlo]")
+            e.salu("s_mov_b32 s85, %[mhi]")
+            e.salu("s_mov_b32 s86, -1")
+            e.salu("s_mov_b32 s87, 0x20000")
+            # sb + DK_W0 + 256 w (lbs = sb + DK_ROWS)
+            e.salu(f"s_lshl_b32 {D_WL}, %[w0], 8")
+            e.salu(f"s_add_u32 {D_WL}, {D_WL}, %[lbs]")
+            e.salu(f"s_add_u32 {D_WL}, {D_WL}, {DK_W0 - DK_ROWS}")
         e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
         e.salu(f"s_mul_i32 {D_LEFT}, %[ng], %[nmt]")  # the block's steps
@@ -1655,7 +1670,7 @@ def gen_dkdv_function(bf16, causal, dropout=False):
     g = DkdvGen(bf16, causal, dropout)
     lines = g.build()
     name = f"dkdv_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_drop' if dropout else ''}"
-    clob = [f'"v{i}"' for i in range(DK_NVGPR_DROP if dropout else DK_NVGPR)] + [f'"a{i}"' for i in range(256)] + \
+    clob = [f'"v{i}"' for i in range(g.nvgpr)] + [f'"a{i}"' for i in range(256)] + \
            [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
     sops = ["ng", "nmt", "c0", "c01", "c012", "mlast", "lq", "qrb"] + ([] if dropout else ["orb"]) + ["qwrap",
