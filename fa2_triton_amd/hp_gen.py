@@ -87,6 +87,45 @@ class Emitter:
         self.rd_ab.clear()
         self.rd_c.clear()
 
+    def _window(self, kind):
+        return {"mfma": self.MFMA_RESULT, "trans": self.TRANS_USE, "m0": self.M0_DMA}.get(
+            kind, max(self.TO_MFMA, self.TO_PERM))
+
+    def close_windows(self):
+        """Pad until no tracked hazard window is open."""
+        need = 0
+        for w, k in self.wr.values():
+            need = max(need, self._window(k) - (self.ws - w))
+        for w in self.rd_ab.values():
+            need = max(need, self.MFMA_READ_WAR - (self.ws - w))
+        for w in self.rd_c.values():
+            need = max(need, self.MFMA_C_WAR - (self.ws - w))
+        self._pad(need)
+
+    def snapshot(self):
+        """Hazard state relative to the current position (a block boundary without a barrier)."""
+        assert not self.ds, "LDS reads pending across a block boundary"
+        return ({r: (self.ws - w, k) for r, (w, k) in self.wr.items()},
+                {r: self.ws - w for r, w in self.rd_ab.items()},
+                {r: self.ws - w for r, w in self.rd_c.items()})
+
+    def restore(self, snaps):
+        """Start a block that may follow any of the blocks whose end states are snaps: per
+        register the most restrictive of them (no barrier in between)."""
+        wr, ab, c = {}, {}, {}
+        for swr, sab, sc in snaps:
+            for r, (rel, k) in swr.items():
+                rem = self._window(k) - rel
+                if rem > 0 and (r not in wr or rem > wr[r][2]):
+                    wr[r] = (rel, k, rem)
+            for src, dst in ((sab, ab), (sc, c)):
+                for r, rel in src.items():
+                    dst[r] = min(rel, dst.get(r, rel))
+        self.ds = []
+        self.wr = {r: (self.ws - rel, k) for r, (rel, k, _) in wr.items()}
+        self.rd_ab = {r: self.ws - rel for r, rel in ab.items()}
+        self.rd_c = {r: self.ws - rel for r, rel in c.items()}
+
     def _need_lgkm(self, regs):
         hit = -1
         for j, dst in enumerate(self.ds):
@@ -1008,15 +1047,38 @@ class FwdGen:
 #   v[160:167]  LSE2 of 8 of the lane's rows (rows of 16-row half sp, reloaded for sp = 1)
 #   a[0:127]    dV^T[kb][dt], a[128:255] dK^T[kb][dt]
 #   K fragments: compiler-placed "v" operands %[k0]..%[k15]
-# LDS (bytes from the workgroup's base): a ring of DK_NBUF = 4 step buffers -- step i reads
-# buffers i and i + 1, its DMA fills buffer i + 3 (two steps of lead): Q tile of buffer b at
-# 16384 b, dO tile at 16384 b + 8192 (Tile<128, 32>), V rows of wave w at DK_V0 + 16384 w
-# (Tile<128, 64>), LSE2 / -delta rows of buffer b at DK_ROWS + 256 b (+128).
-DK_NBUF = 4
-DK_V0 = 16384 * DK_NBUF
-DK_ROWS = DK_V0 + 65536
-DK_LDS = DK_ROWS + 256 * DK_NBUF
-DK_AHEAD = DK_NBUF - 1  # a step's DMA fills the buffer of the step DK_AHEAD later
+# LDS (bytes from the workgroup's base, DkLayout): a ring of nbuf = 5 step buffers -- step i
+# reads buffers i and i + 1, its DMA fills buffer i + 3: Q tile of buffer b at 16384 b, dO tile at
+# 16384 b + 8192 (Tile<128, 32>; buffer 4 through the "h" bases, 64 KiB up: a ds offset has 16
+# bits), V rows of wave w at v0 + 16384 w (Tile<128, 64>), LSE2 / -delta rows of buffer b at
+# rows + 256 b (+128).
+# One barrier per TWO steps (after the odd ones): between the barriers after steps j - 2 and j
+# (j odd) the steps j - 1 and j read buffers j - 1 .. j + 1 and request steps j + 2 and j + 3
+# into the buffers of steps j - 3 and j - 2, which every wave finished reading before the
+# barrier after step j - 2: five buffers.  At that barrier every request so far has landed
+# (vmcnt(0): the odd step's own request is issued early in the step).  The S / P register set
+# alternates per step, so the step bodies come in 10 phases (buffer ph % 5, set ph & 1).
+# The dropout statement keeps four buffers and a barrier after every step (the "h" bases of
+# buffer 4 would spill its VGPRs); FA2_HPGEN_ABL=dk_nb4 gives the plain one the same.
+DK_NBUF_PLAIN = 4 if "dk_nb4" in ABL else 5
+DK_NBUF_DROP = 4
+
+
+class DkLayout:
+    """LDS layout of one dK/dV statement variant (bytes from the workgroup's base)."""
+
+    def __init__(self, nbuf):
+        self.nbuf = nbuf
+        self.ph = nbuf if nbuf % 2 == 0 else 2 * nbuf  # step phases: buffer ph % nbuf, set ph & 1
+        self.halfbar = nbuf == 5
+        self.v0 = 16384 * nbuf
+        self.rows = self.v0 + 65536
+        self.lds = self.rows + 256 * nbuf
+        self.w0 = self.lds  # dropout: keep words of buffer b, wave w at w0 + 1024 b + 256 w
+        self.lds_drop = self.w0 + 1024 * nbuf
+
+
+DK_AHEAD = 3  # a step's DMA fills the buffer of the step DK_AHEAD later
 DK_VMEM = 4  # vector-memory ops of one step's DMA after its rows (the count each step end leaves)
 
 
@@ -1077,8 +1139,12 @@ DKM = [f"v{DK_NVGPR}", f"v{DK_NVGPR + 1}"]
 DTM = [f"v{DK_NVGPR + 2}", f"v{DK_NVGPR + 3}"]
 DK_NVGPR_DROP = DK_NVGPR + 4
 D_MC = "s99"       # dropout: byte offset of the requested step's keep words from the wave's base
-DK_W0 = DK_LDS     # dropout: keep words of buffer b, wave w at DK_W0 + 1024 b + 256 w (64 dwords)
-DK_LDS_DROP = DK_W0 + 1024 * DK_NBUF
+
+
+def _lds_hi(buf, imm, base):
+    """(base operand, offset) of an LDS read at step-buffer offset imm: buffer 4 through the
+    operand's "h" twin (64 KiB up)."""
+    return (base[:-1] + "h]", imm - 65536) if imm >= 65536 else (base, imm)
 
 
 def DDEL(g4, j=None):
@@ -1099,7 +1165,6 @@ def DDK(kb, dt):
 D_G = "s64"        # q-head index in the group
 D_IDX = "s65"      # step index within the head
 D_CM = "s66"       # first query row of the current tile
-D_PAR = "s67"      # step phase i mod DK_NBUF (buffer of step i; S set = phase & 1)
 # descriptors of the requested step's Q, dO, LSE2 and delta rows; their base words ARE the
 # cursors (the requested tile's first byte; stride 0, and a 48-bit address leaves the high
 # word's stride bits clear), word 2 the range of the step, word 3 constant
@@ -1133,6 +1198,7 @@ class DkdvGen:
         self.bf16, self.causal, self.dropout = bf16, causal, dropout
         assert not (dropout and DVF_SLOTS != 4), "the dropout -delta rows use the V ring's 4 slots"
         self.vslots = DVF_SLOTS
+        self.L = DkLayout(DK_NBUF_DROP if dropout else DK_NBUF_PLAIN)
         self.nvgpr = DK_NVGPR_DROP if dropout else DK_NVGPR
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
@@ -1142,7 +1208,7 @@ class DkdvGen:
     def row_read(self, buf, dout, ks):
         """Row fragment ks (Q, or dO when dout) of buffer buf into ring slot ks % 4."""
         imm = buf * 16384 + (8192 if dout else 0) + (ks >> 1) * 2048
-        base = "%[qb1]" if ks & 1 else "%[qb0]"
+        base, imm = _lds_hi(buf, imm, "%[qb1]" if ks & 1 else "%[qb0]")
         d = DRR(ks)
         self.e.ds_read(f"ds_read_b128 {d}, {base} offset:{imm}", d)
 
@@ -1159,7 +1225,7 @@ class DkdvGen:
         buffer buf into the 2 registers dst."""
         sp, dt = f >> 2, f & 3
         imm = buf * 16384 + (8192 if dout else 0) + dt * 2048 + 16 * sp * 64
-        base = "%[tb]" if half else "%[ta]"
+        base, imm = _lds_hi(buf, imm, "%[tb]" if half else "%[ta]")
         self.e.ds_read(f"ds_read_b64_tr_b16 {dst}, {base} offset:{imm}", dst)
 
     def dvf(self, n):
@@ -1182,10 +1248,10 @@ class DkdvGen:
             e.salu(f"s_cselect_b32 {D_T}, {D_T}, 0")
             e.salu(f"s_min_u32 s78, {D_T}, 32")
             e.salu("s_lshl_b32 s78, s78, 2")
-            if self.dropout:  # lsoff = sb + DK_W0 + 256 w + 4 lane (w = 0 here): the range
-                # starts there (lbs = sb + DK_ROWS)
+            if self.dropout:  # lsoff = sb + w0 + 256 w + 4 lane (w = 0 here): the range
+                # starts there (lbs = sb + rows)
                 e.salu("s_add_u32 s78, s78, %[lbs]")
-                e.salu(f"s_add_u32 s78, s78, {DK_W0 - DK_ROWS}")
+                e.salu(f"s_add_u32 s78, s78, {self.L.w0 - self.L.rows}")
             e.salu("s_mov_b32 s82, s78")
         if part in (None, 1):
             orb = "%[qrb]" if self.dropout else "%[orb]"  # (dropout: one row stride)
@@ -1368,12 +1434,24 @@ class DkdvGen:
         self.e.mfma(self.mop, DS(st, kb), DRR(ks), f"%[k{kb * 8 + ks}]", "0" if ks == 0 else DS(st, kb))
 
     # -- one step --------------------------------------------------------------------------------
-    def step(self, par, cls, tag):
-        """Step i with i mod DK_NBUF = par, class A (live, unmasked), B (live, masked) or D (no key
+    def step(self, ph, cls, tag):
+        """Step i with i mod (the layout's phase count) = ph, class A (live, unmasked), B (live, masked) or D (no key
         of the wave visible: only the straddled MFMAs, S(i+1) and the request)."""
         e = self.e
-        st = par & 1           # S / P set of step i; S(i+1) goes to 1 - st
-        nxt = (par + 1) % DK_NBUF
+        L = self.L
+        par = ph % L.nbuf      # buffer of step i
+        st = ph & 1            # S / P set of step i; S(i+1) goes to 1 - st
+        nxt = (ph + 1) % L.nbuf
+        # half barriers: the even step of a pair requests steps i + 3 and i + 4 (the buffers of
+        # steps i - 2 and i - 1, both read before the barrier after step i - 1), the odd one none,
+        # so every request has a whole step to land before the barrier (FA2_HPGEN_ABL=dk_hb1: one
+        # request per step, the odd step's issued early)
+        pair = L.halfbar and "dk_hb1" not in ABL
+        early = L.halfbar and not pair and ph & 1
+        if pair:
+            reqs = [] if ph & 1 else [((par + DK_AHEAD) % L.nbuf, tag), ((par + DK_AHEAD + 1) % L.nbuf, tag + "x")]
+        else:
+            reqs = [((par + DK_AHEAD) % L.nbuf, tag)]
         live = cls in ("A", "B")
         masked = cls == "B"
         if masked and self.causal:
@@ -1384,8 +1462,13 @@ class DkdvGen:
         for ks in range(8):
             rel = 2 * ks + 1
             g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(nxt, False, ks), lds=2)
-        for n, (c, f) in enumerate(self.dma_items((par + DK_AHEAD) % DK_NBUF, tag)):
-            g.add("dma", c, 2 if live else 0, (42 if live else 14) + 3 * n, f)
+        items = [it for nb, t in reqs for it in self.dma_items(nb, t)]
+        for n, (c, f) in enumerate(items):
+            if pair:
+                dl = min(20 + 3 * n, 62) if live else min(6 + n, 23)
+            else:
+                dl = (20 if early and live else 42 if live else 14) + 3 * n
+            g.add("dma", c, 0 if early or not live else 2, dl, f)
         if live:
             # dO(i) row fragments ks (slot ks % 4, after the S MFMAs 2 ks + 17), dP at 24 + 2 ks
             for ks in range(8):
@@ -1535,13 +1618,21 @@ class DkdvGen:
             e._need_lgkm = Emitter._need_lgkm.__get__(e)
         e.drop = None
         e.salu(f"s_sub_u32 {D_CM}, {D_CM}, 32")
-        e.salu(f"s_mov_b32 {D_PAR}, {nxt}")
         e.drain_lds()
-        if "dk_novm" not in ABL:
-            # the next step's tiles (requested two steps ago) have landed; this step's stay in flight
-            e.raw(f"s_waitcnt vmcnt({DK_VMEM})")
-        if "dk_nobar" not in ABL:
-            e.raw("s_barrier")
+        if L.halfbar:
+            if ph & 1:
+                # every request so far (up to step i + 3) has landed
+                e.raw("s_waitcnt vmcnt(0)")
+                e.raw("s_barrier")
+            else:
+                return  # (no reset: the odd step starts from this end state, DkdvGen.build)
+        else:
+            if "dk_novm" not in ABL:
+                # the next step's tiles (requested two steps ago) have landed; this step's stay in
+                # flight
+                e.raw(f"s_waitcnt vmcnt({DK_VMEM})")
+            if "dk_nobar" not in ABL:
+                e.raw("s_barrier")
         e.reset()
 
     def build(self):
@@ -1572,10 +1663,10 @@ class DkdvGen:
             e.salu("s_mov_b32 s85, %[mhi]")
             e.salu("s_mov_b32 s86, -1")
             e.salu("s_mov_b32 s87, 0x20000")
-            # sb + DK_W0 + 256 w (lbs = sb + DK_ROWS)
+            # sb + w0 + 256 w (lbs = sb + rows)
             e.salu(f"s_lshl_b32 {D_WL}, %[w0], 8")
             e.salu(f"s_add_u32 {D_WL}, {D_WL}, %[lbs]")
-            e.salu(f"s_add_u32 {D_WL}, {D_WL}, {DK_W0 - DK_ROWS}")
+            e.salu(f"s_add_u32 {D_WL}, {D_WL}, {self.L.w0 - self.L.rows}")
         e.salu(f"s_mov_b32 {D_NM}, %[mlast]")
         e.salu(f"s_mov_b32 {D_NMT}, 0")
         e.salu(f"s_mul_i32 {D_LEFT}, %[ng], %[nmt]")  # the block's steps
@@ -1593,7 +1684,6 @@ class DkdvGen:
             for _, f in self.dma_items(nb, f"pro{nb}"):
                 f()
         e.salu(f"s_mov_b32 {D_G}, 0")
-        e.salu(f"s_mov_b32 {D_PAR}, 0")
         # no step at all (ng nmt = 0; D_G = 0 here)
         e.raw(f"s_cmp_eq_u32 {D_G}, %[ng]")
         e.raw("s_cbranch_scc1 .Lhp%=_end")
@@ -1611,47 +1701,58 @@ class DkdvGen:
             self.init_read(0, 0, 0, g4)
         e.drain_lds()
         e.drain_mfma()
-        e.raw(f"s_waitcnt vmcnt({DK_VMEM})")  # step 1's tiles
+        # step 1's tiles (half barriers: step 2's too; steps 0 and 1 run before the next barrier)
+        e.raw(f"s_waitcnt vmcnt({0 if self.L.halfbar else DK_VMEM})")
         e.raw("s_barrier")
         e.reset()
-        # head loop
-        e.label(".Lhp%=_head")
         e.salu(f"s_mov_b32 {D_IDX}, 0")
         e.salu(f"s_mov_b32 {D_CM}, %[mlast]")
-        e.raw(".balignl 64, 0xbf800000", 0)
-        e.label(".Lhp%=_step")
-        # class of step IDX: [0, c0) B, [c0, c01) A, [c01, c012) B, then D
-        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c0]")
-        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
-        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c01]")
-        e.raw("s_cbranch_scc1 .Lhp%=_clsA")
-        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c012]")
-        e.raw("s_cbranch_scc1 .Lhp%=_clsB")
-        e.label(".Lhp%=_clsD")
-
-        def dispatch(cls):
-            # step phase D_PAR in 0 .. DK_NBUF - 1 -> the step body of that phase
-            for par in range(DK_NBUF - 1):
-                e.raw(f"s_cmp_eq_u32 {D_PAR}, {par}")
-                e.raw(f"s_cbranch_scc1 .Lhp%=_{cls}{par}")
-            e.raw(f"s_branch .Lhp%=_{cls}{DK_NBUF - 1}")
-
-        dispatch("D")
-        for cls in ("A", "B", "D"):
-            if cls != "D":
-                e.label(f".Lhp%=_cls{cls}")
-                dispatch(cls)
-            for par in range(DK_NBUF):
-                e.label(f".Lhp%=_{cls}{par}")
-                self.step(par, cls, f"{cls.lower()}{par}")
-                e.raw("s_branch .Lhp%=_next")
-        e.label(".Lhp%=_next")
-        e.salu(f"s_add_u32 {D_IDX}, {D_IDX}, 1")
-        e.raw(f"s_cmp_lt_u32 {D_IDX}, %[nmt]")
-        e.raw("s_cbranch_scc1 .Lhp%=_step")
-        e.salu(f"s_add_u32 {D_G}, {D_G}, 1")
-        e.raw(f"s_cmp_lt_u32 {D_G}, %[ng]")
-        e.raw("s_cbranch_scc1 .Lhp%=_head")
+        # one entry per step phase ph: the class of step IDX ([0, c0) B, [c0, c01) A, [c01, c012)
+        # B, then D) -> the body (class, ph); each body continues at the entry of phase ph + 1 (the
+        # phase is static: no dispatch on it)
+        for ph in range(self.L.ph):
+            e.raw(".balignl 64, 0xbf800000", 0)
+            e.label(f".Lhp%=_step{ph}")
+            e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c0]")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_B{ph}")
+            e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c01]")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_A{ph}")
+            e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c012]")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_B{ph}")
+            e.raw(f"s_branch .Lhp%=_D{ph}")
+        snaps = []
+        for ph in range(self.L.ph):
+            ends = []
+            for cls in ("A", "B", "D"):
+                nph = (ph + 1) % self.L.ph
+                e.label(f".Lhp%=_{cls}{ph}")
+                # half barriers: an odd step follows any of the previous phase's bodies with no
+                # barrier between (their merged end states); an even one follows a barrier
+                if self.L.halfbar and ph & 1:
+                    e.restore(snaps)
+                else:
+                    e.reset()
+                self.step(ph, cls, f"{cls.lower()}{ph}")
+                if self.L.halfbar and not ph & 1:
+                    if cls == "D":  # (rare: a head's last steps; its S MFMAs end the body)
+                        e.close_windows()
+                    ends.append(e.snapshot())
+                # next step: within the head, else the next head's first (IDX 0, CM = mlast)
+                e.salu(f"s_add_u32 {D_IDX}, {D_IDX}, 1")
+                e.raw(f"s_cmp_lt_u32 {D_IDX}, %[nmt]")
+                e.raw(f"s_cbranch_scc1 .Lhp%=_step{nph}")
+                e.salu(f"s_add_u32 {D_G}, {D_G}, 1")
+                e.salu(f"s_mov_b32 {D_IDX}, 0")
+                e.salu(f"s_mov_b32 {D_CM}, %[mlast]")
+                e.raw(f"s_cmp_lt_u32 {D_G}, %[ng]")
+                e.raw(f"s_cbranch_scc1 .Lhp%=_step{nph}")
+                e.raw("s_branch .Lhp%=_last")
+            snaps = ends
+        e.label(".Lhp%=_last")
+        # (after any body: every window closed)
+        e.ds = []
+        e._pad(max(Emitter.MFMA_RESULT, Emitter.MFMA_C_WAR))
+        e.reset()
         # the last step's straddled MFMAs
         for m in range(8):
             self.mf_dk_tail(m)
@@ -1676,7 +1777,7 @@ def gen_dkdv_function(bf16, causal, dropout=False):
     sops = ["ng", "nmt", "c0", "c01", "c012", "mlast", "lq", "qrb"] + ([] if dropout else ["orb"]) + ["qwrap",
             "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
             "sc"] + (["kd0"] if causal else []) + (["mlo", "mhi", "mstep", "mwrap"] if dropout else [])
-    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb", "lb", "qoff0", "qoff1"] + ([] if dropout else ["ooff0", "ooff1"]) + \
+    vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb"] + (["qb0h", "qb1h", "tah", "tbh"] if g.L.nbuf > 4 else []) + ["lb", "qoff0", "qoff1"] + ([] if dropout else ["ooff0", "ooff1"]) + \
         ["lsoff"] + (["lr"] if causal else []) + (["dscb"] if dropout else [])
     src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 FA2_DEV void {name}(const u32x4 (&kf)[16], const DkdvHpArgs& a) {{
@@ -2259,6 +2360,15 @@ def write_headers():
             for dropout in (False, True):
                 out.append(gen_dkdv_function(bf16, causal, dropout))
     out.append(gen_read_dkdv())
+    out.append("// LDS layout of the dK/dV statements (DkdvGen, DkLayout): step buffers, V rows at v0, LSE2 /\n"
+               "// -delta rows at rows, the dropout keep words at words; size in bytes\n"
+               "template <bool DROPOUT> struct DkdvLds;")
+    for dropout in (False, True):
+        L = DkLayout(DK_NBUF_DROP if dropout else DK_NBUF_PLAIN)
+        out.append(f"template <> struct DkdvLds<{'true' if dropout else 'false'}> {{\n"
+                   f"  static constexpr int nbuf = {L.nbuf}, v0 = {L.v0}, rows = {L.rows}, words = {L.w0}, "
+                   f"size = {L.lds_drop if dropout else L.lds};\n}};")
+    out.append("")
     out.append("}  // namespace fa2\n")
     paths.append(_write(os.path.join(GEN, "dkdv_hp_body.h"), "\n".join(out)))
     out = ["// generated by fa2_triton_amd/hp_gen.py -- do not edit", "#pragma once", "", "namespace fa2 {", ""]
