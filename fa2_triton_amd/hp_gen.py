@@ -2053,7 +2053,8 @@ class DqGen:
         e.drain_lds()
         if "dq_novm" not in ABL:
             e.raw("s_waitcnt vmcnt(0)")
-        e.raw("s_barrier")
+        if "dq_nobar" not in ABL:
+            e.raw("s_barrier")
         e.reset()
 
     def next_unit_loads(self):
