@@ -28,6 +28,11 @@ BWD_CASES = [
     (1, 2, 2, 777, 333, True, torch.float16),
     (1, 4, 1, 129, 257, False, torch.bfloat16),
     (2, 8, 8, 2048, 2048, True, torch.bfloat16),
+    # dK/dV steps (32 query rows of one q-head) per block: odd totals and 1-3 steps per head, so the
+    # two-step barrier pairs straddle head changes and blocks end on either phase
+    (1, 4, 1, 96, 512, False, torch.bfloat16),
+    (1, 4, 1, 32, 300, True, torch.float16),
+    (2, 3, 1, 160, 160, True, torch.bfloat16),
 ]
 
 
@@ -95,6 +100,7 @@ GRID_CASES = [
     (2, 8, 2, 1024, True, torch.bfloat16, False),
     (2, 8, 8, 1024, False, torch.float16, False),
     (3, 4, 2, 777, True, torch.bfloat16, True),
+    (2, 6, 2, 416, True, torch.bfloat16, False),
 ]
 
 
