@@ -87,9 +87,11 @@ def encode_dtype(x: Tensor) -> int:
 
 
 def bshd_strides(x: Tensor) -> Tuple[int, int, int]:
-    """(batch, seq, head) element strides of a [B, S, H, D] view with unit last stride."""
-    assert x.stride(-1) == 1, "last dimension must be contiguous"
-    return x.stride(0), x.stride(1), x.stride(2)
+    """(batch, seq, head) element strides of a [B, S, H, D] view with unit last stride (one
+    stride() call: each costs ~0.4 us of host time, and a launch makes four of these)."""
+    s = x.stride()
+    assert s[-1] == 1, "last dimension must be contiguous"
+    return s[0], s[1], s[2]
 
 
 def stream_of(x: Tensor) -> int:
