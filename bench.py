@@ -303,7 +303,7 @@ def resolve(args):
     if args.warmup is None:
         # untimed warm-up of >= ~20 ms of GPU work, so the timed region starts at the sustained
         # clock (cfg3's 5 steps are 21 ms; five 46-us cfg2 steps would leave it ramping up)
-        args.warmup = 400 if args.config == "cfg2" else 5
+        args.warmup = {"cfg2": 400, "refbench": 25}.get(args.config, 5)
     for key in ("batch", "heads", "heads_kv", "seqlen", "head_dim", "dtype"):
         if getattr(args, key) is None:
             setattr(args, key, preset[key])
@@ -319,7 +319,7 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg3")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; 1000 for cfg2's 46 us step)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; 400 for cfg2)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; 400 for cfg2, 25 for refbench)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (weak scaling)")
     ap.add_argument("--strong", action="store_true", help="split --global-batch over the GPUs")
     ap.add_argument("--global-batch", type=int, default=64)
