@@ -12,7 +12,10 @@ forward + one backward of that batch.  The other BASELINE configs have presets t
 and every field can be overridden (--batch --heads --heads-kv --seqlen --head-dim --dtype
 --no-causal --fwd-only).  `--bias` adds the reference tests' additive bias (a [1, 1, Sq, Sk]
 tensor in the input dtype, /root/reference/tests/core.py:28) and `--dropout P` dropout with a
-fixed seed: both leave the algorithmic FLOPs unchanged and run the non-pipelined kernels.
+fixed seed: both leave the algorithmic FLOPs unchanged (dropout runs the general forward and the
+hand-placed dQ / dK/dV over the saved keep words; a 16-bit bias the pipelined forward and the
+general backward kernels).  Warm-up (untimed) defaults to >= ~20 ms of GPU work so the timed
+region starts at the sustained clock: 5 steps, 25 for refbench, 400 for cfg2 (1000 timed).
 
 Multi-GPU (BASELINE.json configs[3]: B=64 over 8 GPUs): one process
 per GPU, each running its own batch shard with no collective on the data path.  The ranks meet
