@@ -505,13 +505,17 @@ def main():
     workload_ok = (b, h, hkv, s, d, causal, dtype, fwd_only, plain) == (8, 32, 32, 4096, 128, True, torch.bfloat16, False,
                                                                        True)
     dominant = max(times, key=lambda n: times[n])
-    # device symbols the workload dispatches to (the hand-placed kernels: D = 128, aligned, no bias,
-    # no dropout -- the dropout dQ also, with the saved keep words)
-    hp_fwd = hp_dkdv = plain and d == 128
-    hp_dq = d == 128 and d % 8 == 0 and bias is None
-    symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if plain else "fwd_kernel"),
-              "dkdv_kernel": "dkdv_hp_kernel" if hp_dkdv else "dkdv_kernel",
-              "dq_kernel": "dq_hp_kernel" if hp_dq else "dq_kernel", "dbias_kernel": "dbias_kernel"}
+    # device symbols the workload dispatches to, by the library's own conditions (the bench's tensors
+    # are contiguous, so every row is 16-byte aligned): forward -- fwd_hp_ok (D = 128, no bias, no
+    # dropout), else fwd_pipe_kernel (D in {64, 128}, no dropout, no bias or a 16-bit one:
+    # bias16_rows), else fwd_kernel; dQ / dK-dV -- dq_hp_ok / dkdv_hp_ok (D = 128, no bias; with
+    # dropout only through the forward's saved keep words, which this bench passes)
+    hp_fwd = d == 128 and bias is None and p_drop == 0.0
+    pipe_fwd = d in (64, 128) and p_drop == 0.0 and (bias is None or bias.dtype in (torch.float16, torch.bfloat16))
+    hp_bwd = d == 128 and bias is None
+    symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if pipe_fwd else "fwd_kernel"),
+              "dkdv_kernel": "dkdv_hp_kernel" if hp_bwd else "dkdv_kernel",
+              "dq_kernel": "dq_hp_kernel" if hp_bwd else "dq_kernel", "dbias_kernel": "dbias_kernel"}
     esz = q.element_size()
 
     def roofline(name):

@@ -103,16 +103,48 @@ class BwdArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 8  # FA2_ABI_VERSION in include/fa2_amd.h
+class Policy(ctypes.Structure):
+    """Mirror of fa2_policy (include/fa2_amd.h, ABI 9): the kernel-path policy of one call."""
 
-EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_dkv_workspace_bytes", "fa2_dropout_mask_bytes",
-                    "fa2_cu_seqlens_from_mask", "fa2_set_path_policy",
+    _fields_ = [("disable", ctypes.c_uint32), ("grid_cap", ctypes.c_int32)]
+
+
+ABI_VERSION = 9  # FA2_ABI_VERSION in include/fa2_amd.h
+
+EXPORTED_SYMBOLS = ("fa2_fwd", "fa2_fwd_ex", "fa2_bwd", "fa2_bwd_stages", "fa2_bwd_stages_ex",
+                    "fa2_bwd_dkv_workspace_bytes", "fa2_dropout_mask_bytes", "fa2_cu_seqlens_from_mask",
                     "fa2_last_error", "fa2_version")
-# fa2_path bits (fa2_set_path_policy)
+# fa2_path bits (fa2_policy.disable)
 PATH_FWD_HP, PATH_DQ_HP, PATH_DKDV_HP = 1, 2, 4
 
 _lock = threading.Lock()
 _lib = None
+
+
+def bind(lib: ctypes.CDLL) -> ctypes.CDLL:
+    """Declare the argument and result types of every exported function on `lib`."""
+    lib.fa2_fwd.argtypes = [ctypes.POINTER(FwdArgs), ctypes.c_void_p]
+    lib.fa2_fwd.restype = ctypes.c_int
+    lib.fa2_bwd.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_void_p]
+    lib.fa2_bwd.restype = ctypes.c_int
+    lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.c_void_p]
+    lib.fa2_bwd_stages.restype = ctypes.c_int
+    lib.fa2_bwd_dkv_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
+    lib.fa2_bwd_dkv_workspace_bytes.restype = ctypes.c_int64
+    lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+    lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int
+    lib.fa2_last_error.argtypes = []
+    lib.fa2_last_error.restype = ctypes.c_char_p
+    lib.fa2_dropout_mask_bytes.argtypes = [ctypes.c_int32] * 4
+    lib.fa2_dropout_mask_bytes.restype = ctypes.c_int64
+    lib.fa2_fwd_ex.argtypes = [ctypes.POINTER(FwdArgs), ctypes.POINTER(Policy), ctypes.c_void_p]
+    lib.fa2_fwd_ex.restype = ctypes.c_int
+    lib.fa2_bwd_stages_ex.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.POINTER(Policy), ctypes.c_void_p]
+    lib.fa2_bwd_stages_ex.restype = ctypes.c_int
+    lib.fa2_version.argtypes = []
+    lib.fa2_version.restype = ctypes.c_int
+    return lib
 
 
 def load() -> ctypes.CDLL:
@@ -128,26 +160,7 @@ def load() -> ctypes.CDLL:
                 f"fa2_triton_amd: HIP library not found at {LIB_PATH}; build it with "
                 "`python -m fa2_triton_amd.build` (hipcc --offload-arch=gfx950)"
             )
-        lib = ctypes.CDLL(LIB_PATH)
-        lib.fa2_fwd.argtypes = [ctypes.POINTER(FwdArgs), ctypes.c_void_p]
-        lib.fa2_fwd.restype = ctypes.c_int
-        lib.fa2_bwd.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_void_p]
-        lib.fa2_bwd.restype = ctypes.c_int
-        lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(BwdArgs), ctypes.c_int, ctypes.c_void_p]
-        lib.fa2_bwd_stages.restype = ctypes.c_int
-        lib.fa2_bwd_dkv_workspace_bytes.argtypes = [ctypes.POINTER(BwdArgs)]
-        lib.fa2_bwd_dkv_workspace_bytes.restype = ctypes.c_int64
-        lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                                 ctypes.c_void_p, ctypes.c_void_p]
-        lib.fa2_cu_seqlens_from_mask.restype = ctypes.c_int
-        lib.fa2_last_error.argtypes = []
-        lib.fa2_last_error.restype = ctypes.c_char_p
-        lib.fa2_dropout_mask_bytes.argtypes = [ctypes.c_int32] * 4
-        lib.fa2_dropout_mask_bytes.restype = ctypes.c_int64
-        lib.fa2_set_path_policy.argtypes = [ctypes.c_uint32, ctypes.c_int32]
-        lib.fa2_set_path_policy.restype = ctypes.c_int
-        lib.fa2_version.argtypes = []
-        lib.fa2_version.restype = ctypes.c_int
+        lib = bind(ctypes.CDLL(LIB_PATH))
         version = lib.fa2_version()
         if version != ABI_VERSION:
             raise RuntimeError(f"fa2_triton_amd: library ABI version {version}, expected {ABI_VERSION}")
@@ -167,7 +180,31 @@ def check(rc: int) -> None:
     raise RuntimeError(f"fa2_triton_amd: {msg} (status {rc})")
 
 
+# The kernel-path policy the host layer passes with each call (fa2_fwd_ex / fa2_bwd_stages_ex):
+# a test / A/B hook of this Python layer, (0, 0) = the defaults.  The library itself keeps no
+# state between calls (ABI 9); a module variable rather than a thread-local one so that it also
+# reaches the backward, which autograd runs on its own device thread.
+_policy = Policy(0, 0)
+
+
 def set_path_policy(disable: int = 0, grid_cap: int = 0) -> None:
-    """fa2_set_path_policy: turn the hand-placed paths named by `disable` (PATH_* bits) off and cap
-    the persistent kernels' grid (0: one workgroup per CU).  (0, 0) restores the defaults."""
-    check(load().fa2_set_path_policy(disable, grid_cap))
+    """Turn the hand-placed paths named by `disable` (PATH_* bits) off and cap the persistent
+    kernels' grid (0: one workgroup per CU) for the following calls of this process.  (0, 0)
+    restores the defaults."""
+    if disable & ~(PATH_FWD_HP | PATH_DQ_HP | PATH_DKDV_HP):
+        raise ValueError(f"unknown path bits {disable:#x}")
+    if grid_cap < 0:
+        raise ValueError(f"grid_cap {grid_cap} < 0")
+    _policy.disable, _policy.grid_cap = disable, grid_cap
+
+
+def fwd(args: FwdArgs, stream) -> int:
+    """fa2_fwd_ex with the host layer's policy (NULL when it is the default)."""
+    pol = ctypes.byref(_policy) if (_policy.disable or _policy.grid_cap) else None
+    return load().fa2_fwd_ex(ctypes.byref(args), pol, stream)
+
+
+def bwd_stages(args: BwdArgs, stages: int, stream) -> int:
+    """fa2_bwd_stages_ex with the host layer's policy (NULL when it is the default)."""
+    pol = ctypes.byref(_policy) if (_policy.disable or _policy.grid_cap) else None
+    return load().fa2_bwd_stages_ex(ctypes.byref(args), stages, pol, stream)

@@ -133,8 +133,7 @@ def _flash_attn_backward(
     if dkv_ws is not None:
         args.dkv_workspace, args.dkv_workspace_bytes = dkv_ws.data_ptr(), dkv_ws.numel()
     stages = _stages if _stages is not None else (14 if bias_grad else 6)
-    lib = _lib.load()
-    _lib.check(launch_on(q, lambda st: lib.fa2_bwd_stages(ctypes.byref(args), stages, st)))
+    _lib.check(launch_on(q, lambda st: _lib.bwd_stages(args, stages, st)))
     if not bias_grad:
         return dq, dk, dv
     return dq, dk, dv, dbias32.view(bias.shape).to(bias.dtype)

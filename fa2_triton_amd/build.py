@@ -97,7 +97,23 @@ def compile_one(src: str, force: bool, dep_t: float) -> str:
     return obj
 
 
+DEFAULT_LIB = os.path.join(HERE, "libfa2_amd.so")
+
+
+def check_dev_env():
+    """Development builds (timing ablations FA2_HPGEN_ABL, whose outputs are wrong; the stamp or
+    dev variants -DFA2_HP_STAMPS / -DFA2_HP_DEV) never overwrite the shipped library or its objects."""
+    dev = [k for k in ("FA2_HPGEN_ABL",) if os.environ.get(k)]
+    flags = os.environ.get("FA2_HIPCC_FLAGS", "")
+    dev += [f for f in ("FA2_HP_STAMPS", "FA2_HP_DEV") if f in flags]
+    if dev and (os.path.abspath(LIB) == os.path.abspath(DEFAULT_LIB) or
+                os.path.abspath(OBJ) == os.path.abspath(os.path.join(HERE, "_build"))):
+        raise RuntimeError(f"development build ({', '.join(dev)}) must set FA2_LIB_OUT and FA2_BUILD_DIR away from "
+                           f"the shipped library ({DEFAULT_LIB}) and its objects")
+
+
 def build(force: bool = False, jobs: int = 0) -> str:
+    check_dev_env()
     os.makedirs(OBJ, exist_ok=True)
     generated_headers()
     srcs = [os.path.join(CSRC, "api.hip"), os.path.join(CSRC, "misc.hip")] + generated_sources()

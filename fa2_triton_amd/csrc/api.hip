@@ -69,9 +69,25 @@ hipError_t dispatch_dt(int dt, F4 f32, F8 f64, F12 f128, F16 f256) {
 }  // namespace
 
 namespace fa2 {
-volatile uint32_t g_path_disable = 0;
-volatile int32_t g_grid_cap = 0;
+// the policy of the fa2_*_ex call running on this thread (nullptr: defaults); set only for the
+// duration of that call (PolicyScope), so the library keeps no state between calls
+thread_local const fa2_policy* g_call_policy = nullptr;
 }  // namespace fa2
+
+namespace {
+struct PolicyScope {
+  const fa2_policy* prev;
+  explicit PolicyScope(const fa2_policy* p) : prev(fa2::g_call_policy) { fa2::g_call_policy = p; }
+  ~PolicyScope() { fa2::g_call_policy = prev; }
+};
+int check_policy(const fa2_policy* p) {
+  if (!p) return FA2_OK;
+  if (p->disable & ~(uint32_t)(FA2_PATH_FWD_HP | FA2_PATH_DQ_HP | FA2_PATH_DKDV_HP))
+    return fail(FA2_E_INVALID, "unknown path bits 0x%x", p->disable);
+  if (p->grid_cap < 0) return fail(FA2_E_INVALID, "grid_cap %d < 0", p->grid_cap);
+  return FA2_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -79,17 +95,12 @@ int fa2_version(void) { return FA2_ABI_VERSION; }
 
 const char* fa2_last_error(void) { return g_err; }
 
-int fa2_set_path_policy(uint32_t disable, int32_t grid_cap) {
-  if (disable & ~(uint32_t)(FA2_PATH_FWD_HP | FA2_PATH_DQ_HP | FA2_PATH_DKDV_HP))
-    return fail(FA2_E_INVALID, "unknown path bits 0x%x", disable);
-  if (grid_cap < 0) return fail(FA2_E_INVALID, "grid_cap %d < 0", grid_cap);
-  fa2::g_path_disable = disable;
-  fa2::g_grid_cap = grid_cap;
-  return FA2_OK;
-}
+int fa2_fwd(const fa2_fwd_args* a, void* stream) { return fa2_fwd_ex(a, nullptr, stream); }
 
-int fa2_fwd(const fa2_fwd_args* a, void* stream) {
+int fa2_fwd_ex(const fa2_fwd_args* a, const fa2_policy* policy, void* stream) {
   if (!a) return fail(FA2_E_INVALID, "null args");
+  if (int prc = check_policy(policy)) return prc;
+  PolicyScope scope(policy);
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
   if (rc) return rc;
@@ -119,8 +130,12 @@ int fa2_fwd(const fa2_fwd_args* a, void* stream) {
   return hip_status(e, "fa2_fwd launch");
 }
 
-int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) {
+int fa2_bwd_stages(const fa2_bwd_args* a, int stages, void* stream) { return fa2_bwd_stages_ex(a, stages, nullptr, stream); }
+
+int fa2_bwd_stages_ex(const fa2_bwd_args* a, int stages, const fa2_policy* policy, void* stream) {
   if (!a) return fail(FA2_E_INVALID, "null args");
+  if (int prc = check_policy(policy)) return prc;
+  PolicyScope scope(policy);
   int rc = check_common(a->batch, a->heads_q, a->heads_kv, a->seqlen_q, a->seqlen_k, a->head_dim, a->dtype,
                         a->lse_row_stride, a->cu_seqlens, a->dropout_p);
   if (rc) return rc;

@@ -6,11 +6,14 @@
 
 namespace fa2 {
 
-// fa2_set_path_policy (api.hip): bits of fa2_path disabled, persistent-grid cap (0: none)
-extern volatile uint32_t g_path_disable;
-extern volatile int32_t g_grid_cap;
-inline bool path_on(uint32_t bit) { return !(g_path_disable & bit); }
-inline int capped_grid(int ncu) { const int c = g_grid_cap; return c > 0 && c < ncu ? c : ncu; }
+// the fa2_policy of the fa2_fwd_ex / fa2_bwd_stages_ex call running on this thread, nullptr for
+// the defaults (api.hip; set for the duration of that call only)
+extern thread_local const fa2_policy* g_call_policy;
+inline bool path_on(uint32_t bit) { return !(g_call_policy && (g_call_policy->disable & bit)); }
+inline int capped_grid(int ncu) {
+  const int c = g_call_policy ? g_call_policy->grid_cap : 0;
+  return c > 0 && c < ncu ? c : ncu;
+}
 
 // Forward, one translation unit per (dtype, head-dim tile); see fwd_inst.hip.
 template <bool BF16, int DT>

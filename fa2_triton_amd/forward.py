@@ -8,7 +8,6 @@ HIP kernel reads the padded tensors in place using device-side cu_seqlens.  Keyw
 `dropout_mask` (beyond the reference): an int32 buffer of dropout_mask_words(...) words that the
 forward fills with the keep bits it drew, for the backward to read instead of regenerating them.
 """
-import ctypes
 import math
 from typing import Optional, Tuple
 
@@ -79,6 +78,5 @@ def _flash_attn_forward(
     if dropout_mask is not None and dropout_p > 0.0:
         check_dropout_mask(dropout_mask, batch, nheads_q, seqlen_q, seqlen_k, q.device)
         args.dropout_mask = dropout_mask.data_ptr()
-    lib = _lib.load()
-    _lib.check(launch_on(q, lambda st: lib.fa2_fwd(ctypes.byref(args), st)))
+    _lib.check(launch_on(q, lambda st: _lib.fwd(args, st)))
     return o, lse, softmax_scale, dropout_seed

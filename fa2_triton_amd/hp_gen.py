@@ -226,6 +226,8 @@ class Emitter:
             self.wr["m0"] = (self.ws, "m0")
 
     def dma(self, text):
+        if self.drop and self.drop.search(text):
+            return
         self._hazards("dma", {"m0"}, set())
         self._line(text)
 
@@ -594,22 +596,36 @@ class FwdGen:
         self.rescale(st)
         e.label(f".Lhp%=_{tag}_nr")
 
+    # -- s_memtime stamps (FA2_HP_STAMPS development builds only) ---------------------------------
+    # per period: s[96:97] = its start (after the previous barrier), s[92:93] = the start of phase
+    # Y (PV), s[94:95] = its end before the period-end waits; sums: s98 = phase X cycles, s99 =
+    # phase Y + tail, %[st2] = prologue wait + every period-end wait and barrier
+    def stamp_end_pre(self):
+        e = self.e
+        e.raw("s_memtime s[94:95]")
+        e.drain_lds()
+        e.raw("s_waitcnt lgkmcnt(0)")
+        e.raw("s_sub_u32 s93, s94, s92")
+        e.raw("s_add_u32 s99, s99, s93")
+        e.raw("s_sub_u32 s92, s92, s96")
+        e.raw("s_add_u32 s98, s98, s92")
+
+    def stamp_end_post(self):
+        e = self.e
+        e.raw("s_memtime s[96:97]")
+        e.raw("s_waitcnt lgkmcnt(0)")
+        e.raw("s_sub_u32 s92, s96, s94")
+        e.raw("s_add_u32 %[st2], %[st2], s92")
+
     def barrier(self):
         e = self.e
-        if self.stamp:  # s98 += wait for own LDS reads + DMA, s99 += barrier (dev builds only)
-            e.raw("s_memtime s[92:93]")
+        if self.stamp:
+            self.stamp_end_pre()
         e.drain_lds()
         e.raw("s_waitcnt vmcnt(0)")
-        if self.stamp:
-            e.raw("s_memtime s[94:95]")
         e.raw("s_barrier")
         if self.stamp:
-            e.raw("s_memtime s[96:97]")
-            e.raw("s_waitcnt lgkmcnt(0)")
-            e.raw("s_sub_u32 s92, s94, s92")
-            e.raw("s_add_u32 s98, s98, s92")
-            e.raw("s_sub_u32 s92, s96, s94")
-            e.raw("s_add_u32 s99, s99, s92")
+            self.stamp_end_post()
         e.reset()
 
     # -- phases --------------------------------------------------------------------------------
@@ -652,10 +668,14 @@ class FwdGen:
         e.salu(f"s_add_i32 {SN1}, {SN1}, 64")
         e.salu(f"s_xor_b32 {SPAR}, {SPAR}, 1")
         if final:
+            if self.stamp:
+                self.stamp_end_pre()
             # the next unit's loads stay in flight across the epilogue (its statement waits)
             e.drain_lds()
             e.raw(f"s_waitcnt vmcnt({3 * self.np + 2 * self.ks})")
             e.raw("s_barrier")
+            if self.stamp:
+                self.stamp_end_post()
             e.reset()
         else:
             self.barrier()
@@ -773,10 +793,18 @@ class FwdGen:
             d = S(nxt, rb, t)
             e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * self.ks + ks}]", self.chain0(rb) if ks == 0 else d)
 
+        # development timing ablations of the steady-state (class A) period: FA2_HPGEN_ABL=fw_*
+        # (wrong outputs; cycles only, read with the stamp build)
+        drops = {"fw_nodma": r"^buffer_load|^s_add_u32 m0", "fw_noexp": r"^v_exp",
+                 "fw_novalu": r"^v_(?!mfma)", "fw_nolds": r"^ds_read", "fw_nosalu": r"^s_(?!waitcnt|barrier|cbranch|nop|branch)"}
+        pat = "|".join(v for k, v in drops.items() if k in ABL) if cls == "A" else ""
+        e.drop = re.compile(pat) if pat else None
         if qk:
             for m in range(LEADK):
                 self.k_read(kbuf, m)
         gx.run(x_mfma, pre_budget=40)
+        if self.stamp:
+            e.raw("s_memtime s[92:93]")
         # ---------------- phase Y ----------------
         nv = 4 * self.ndt       # V^T fragments per tile (two MFMAs each)
         ny = 2 * nv             # phase Y MFMAs (32 at D = 128)
@@ -826,6 +854,7 @@ class FwdGen:
         if qk:
             self.row_max_finish()
             self.vote_and_rescale(nxt, tag)
+        e.drop = None
         self.period_end(final)
 
     def dma_stream(self, par):
@@ -848,6 +877,8 @@ class FwdGen:
         return out
 
     def period_d(self, par, final=False):
+        if self.stamp:
+            self.e.raw("s_memtime s[92:93]")
         if final:
             items = self.next_unit_items(par)
         else:
@@ -901,7 +932,7 @@ class FwdGen:
         # or before the statement) have landed
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
         e.raw("s_barrier")
-        if self.stamp:  # prologue wait
+        if self.stamp:  # prologue wait (st2 then adds every period-end wait)
             e.raw("s_memtime s[92:93]")
             e.raw("s_waitcnt lgkmcnt(0)")
             e.raw("s_sub_u32 s92, s92, s100")
@@ -930,6 +961,9 @@ class FwdGen:
         e.label(".Lhp%=_pro_end")
         e.drain_mfma()
         e.raw("s_barrier")  # every wave is done with K(0) before K(2) lands in its buffer
+        if self.stamp:  # the first period starts here
+            e.raw("s_memtime s[96:97]")
+            e.raw("s_waitcnt lgkmcnt(0)")
         e.reset()
         e.salu(f"s_mov_b32 {SN1}, 64")
         e.salu("s_add_i32 s67, %[ntiles], -1")  # s67: index of the final period

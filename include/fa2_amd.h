@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define FA2_ABI_VERSION 8
+#define FA2_ABI_VERSION 9
 
 /* dtype codes: same numbers as the reference's encode_dtype (src/utils.py:102-109). */
 enum fa2_dtype { FA2_F16 = 16, FA2_BF16 = 17, FA2_F32 = 32 };
@@ -166,16 +166,21 @@ int64_t fa2_dropout_mask_bytes(int32_t batch, int32_t heads_q, int32_t seqlen_q,
 int fa2_cu_seqlens_from_mask(const uint8_t* mask, int64_t mask_row_stride, int32_t batch,
                              int32_t seqlen, int32_t* cu_seqlens, void* stream);
 
-/* Kernel-path policy (ABI 7), process-wide, read at every launch; for tests and A/B timing.
- * Bits of `disable` turn a specialised path off so that the general kernels of the same launch
- * run instead (same math; the tests compare the two): FA2_PATH_FWD_HP the hand-placed D = 128
- * forward, FA2_PATH_DQ_HP / FA2_PATH_DKDV_HP the hand-placed D = 128 dQ / dK-dV.
- * grid_cap > 0 caps the grid of the persistent (one workgroup per CU) kernels, so that small
- * problems run several work units per workgroup.  Default (0, 0): every path on, one workgroup
- * per CU.  Not synchronised with launches in flight on other threads.  The environment is
- * never read. */
+/* Kernel-path policy of ONE call (ABI 9; replaces ABI 7's process-wide fa2_set_path_policy: the
+ * library keeps no mutable state between calls), for tests and A/B timing.  Bits of `disable`
+ * turn a specialised path off so that the general kernels of the same launch run instead (same
+ * math; the tests compare the two): FA2_PATH_FWD_HP the hand-placed D = 128 forward,
+ * FA2_PATH_DQ_HP / FA2_PATH_DKDV_HP the hand-placed D = 128 dQ / dK-dV.  grid_cap > 0 caps the
+ * grid of the persistent (one workgroup per CU) kernels, so that small problems run several work
+ * units per workgroup.  A NULL policy, or {0, 0}, is the default: every path on, one workgroup
+ * per CU (fa2_fwd / fa2_bwd_stages).  The environment is never read. */
 enum fa2_path { FA2_PATH_FWD_HP = 1, FA2_PATH_DQ_HP = 2, FA2_PATH_DKDV_HP = 4 };
-int fa2_set_path_policy(uint32_t disable, int32_t grid_cap);
+typedef struct fa2_policy {
+  uint32_t disable;  /* fa2_path bits */
+  int32_t grid_cap;  /* 0: no cap */
+} fa2_policy;
+int fa2_fwd_ex(const fa2_fwd_args* args, const fa2_policy* policy, void* stream);
+int fa2_bwd_stages_ex(const fa2_bwd_args* args, int stages, const fa2_policy* policy, void* stream);
 
 const char* fa2_last_error(void);
 int fa2_version(void);

@@ -21,11 +21,7 @@ envs = {}
 for arg in sys.argv[1:]:
     path, _, env = arg.partition(":")
     lib = ctypes.CDLL(os.path.abspath(path))
-    lib.fa2_fwd.argtypes = [ctypes.POINTER(L.FwdArgs), ctypes.c_void_p]
-    lib.fa2_bwd_stages.argtypes = [ctypes.POINTER(L.BwdArgs), ctypes.c_int, ctypes.c_void_p]
-    lib.fa2_cu_seqlens_from_mask.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                             ctypes.c_void_p, ctypes.c_void_p]
-    lib.fa2_last_error.restype = ctypes.c_char_p
+    lib = L.bind(lib)
     name = os.path.basename(path) + (":" + env if env else "")
     envs[name] = dict(kv.split("=", 1) for kv in env.split(",")) if env else {}
     libs.append((name, lib))

@@ -1,4 +1,4 @@
-"""Same-process A/B of the hand-placed kernels against the general ones (fa2_set_path_policy):
+"""Same-process A/B of the hand-placed kernels against the general ones (_lib.set_path_policy: the per-call fa2_policy):
 forward times for a few shapes.  usage: python scripts/ab_policy.py [D]"""
 import sys
 

@@ -17,9 +17,7 @@ from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
 
 def load(arg):
     path, _, env = arg.partition(":")
-    lib = ctypes.CDLL(os.path.abspath(path))
-    lib.fa2_fwd.argtypes = [ctypes.POINTER(L.FwdArgs), ctypes.c_void_p]
-    lib.fa2_last_error.restype = ctypes.c_char_p
+    lib = L.bind(ctypes.CDLL(os.path.abspath(path)))
     return lib, dict(kv.split("=", 1) for kv in env.split(",")) if env else {}
 
 

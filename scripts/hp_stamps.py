@@ -1,41 +1,44 @@
-"""Where a hand-placed kernel's time goes, from s_memtime stamps (dev tool).
+"""Where the hand-placed forward's time goes, from s_memtime stamps (dev tool).
 
-Needs the stamp build:  FA2_HIPCC_FLAGS=-DFA2_HP_STAMPS=1 FA2_BUILD_DIR=fa2_triton_amd/_build_stamps
-FA2_LIB_OUT=fa2_triton_amd/libfa2_amd_stamps.so python -m fa2_triton_amd.build
-Run: python scripts/hp_stamps.py   (loads libfa2_amd_stamps.so through FA2_AMD_LIB)
-Per wave and unit (cycles of the shader clock): the statement, its prologue wait, the period-end
-waits (own LDS reads + DMA), the barrier waits, and the epilogue after the statement.
+Needs a stamp build (scripts/fwd_stamp_abl.sh builds them, with optional timing ablations):
+  FA2_HIPCC_FLAGS=-DFA2_HP_STAMPS=1 ... -> ab_libs/NAME.so
+Run: python scripts/hp_stamps.py ab_libs/NAME.so [...]   (each library in a child process)
+Per wave and unit (cycles of the shader clock): the statement, its phases -- X (QK^T(i+1) with the
+exponentials of tile i: from the period start to the first PV MFMA's region), Y (PV(i) with the row
+sums and the next tile's mask / row max, then the vote), the period-end waits + barrier (plus the
+unit's prologue wait) -- and the epilogue after the statement.
 """
 import ctypes
 import json
 import os
+import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-os.environ.setdefault("FA2_AMD_LIB", os.path.join(HERE, "..", "fa2_triton_amd", "libfa2_amd_stamps.so"))
-sys.path.insert(0, os.path.dirname(HERE))
-
-import torch  # noqa: E402
-
-from fa2_triton_amd import _lib  # noqa: E402
-from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
-
-lib = _lib.load()
-rd = lib.fa2_debug_hp_stamps
-rd.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 
 
-def stamps():
-    buf = (ctypes.c_ulonglong * 16)()
-    assert rd(buf) == 0
-    return list(buf)
+def run_one(lib_path, cases):
+    os.environ["FA2_AMD_LIB"] = os.path.abspath(lib_path)
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
 
+    from fa2_triton_amd import _lib
+    from fa2_triton_amd.forward import _flash_attn_forward
 
-for causal in (True, False):
-    for S, B in ((4096, 8), (16384, 2)):
+    lib = _lib.load()
+    rd = lib.fa2_debug_hp_stamps
+    rd.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+
+    def stamps():
+        buf = (ctypes.c_ulonglong * 16)()
+        assert rd(buf) == 0
+        return list(buf)
+
+    for causal, S, B in cases:
         torch.manual_seed(0)
         q, k, v = (torch.randn(B, S, 32, 128, device="cuda", dtype=torch.bfloat16) * 0.5 for _ in range(3))
-        _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        for _ in range(3):
+            _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
         torch.cuda.synchronize()
         stamps()
         reps = 5
@@ -46,17 +49,30 @@ for causal in (True, False):
         e1.record()
         torch.cuda.synchronize()
         st = stamps()
-        units = st[5] / 4  # per wave
         nmb = S // 256
         tiles = B * 32 * (sum(mb + 1 for mb in range(nmb)) * 4 if causal else nmb * S // 64) * reps
-        rec = {"kernel": "fwd_hp", "S": S, "B": B, "causal": causal, "ms": round(e0.elapsed_time(e1) / reps, 4),
-               "units_per_wave_launches": units / reps}
-        for name, i in (("dma_lds_wait", 0), ("barrier_wait", 1), ("prologue_wait", 2), ("statement", 3), ("epilogue", 4)):
-            rec[name + "_cyc_per_unit"] = round(st[i] / st[5], 1)
-        rec["periods_per_unit"] = round(tiles / (st[5] / 4), 2)
-        rec["statement_cyc_per_period"] = round(st[3] / st[5] / rec["periods_per_unit"], 1)
-        rec["dma_lds_wait_frac"] = round(st[0] / st[3], 4)
-        rec["barrier_wait_frac"] = round(st[1] / st[3], 4)
-        rec["prologue_wait_frac"] = round(st[2] / st[3], 4)
-        rec["epilogue_over_statement"] = round(st[4] / st[3], 4)
+        waves = st[5]  # units x waves
+        periods = tiles / (waves / 4)
+        rec = {"lib": os.path.basename(lib_path), "S": S, "B": B, "causal": causal,
+               "ms": round(e0.elapsed_time(e1) / reps, 4), "periods_per_unit": round(periods, 2)}
+        for name, i in (("phase_x", 0), ("phase_y", 1), ("waits", 2), ("statement", 3), ("epilogue", 4)):
+            rec[name + "_cyc_per_period"] = round(st[i] / waves / periods, 1)
+        rec["rest_cyc_per_unit"] = round((st[3] - st[0] - st[1] - st[2]) / waves, 1)
+        rec["epilogue_cyc_per_unit"] = round(st[4] / waves, 1)
+        # cycles per SIMD per launch (one wave per SIMD) over the launch time: the in-kernel clock
+        rec["clock_ghz"] = round((st[3] + st[4]) / 1024 / reps / (rec["ms"] * 1e6), 3)
         print(json.dumps(rec), flush=True)
+
+
+CASES = [(False, 4096, 8), (False, 16384, 2), (True, 4096, 8)]
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 or (len(sys.argv) == 2 and sys.argv[1] != "--child"):
+        rc = 0
+        for lib in sys.argv[1:]:
+            r = subprocess.run([sys.executable, __file__, "--child"], env=dict(os.environ, FA2_STAMP_LIB=lib))
+            rc = rc or r.returncode
+            if r.returncode:
+                break
+        sys.exit(rc)
+    run_one(os.environ.get("FA2_STAMP_LIB", os.path.join(HERE, "..", "fa2_triton_amd", "libfa2_amd_stamps.so")), CASES)

@@ -1,6 +1,6 @@
 """GPU dev check of the hand-placed forward (fwd_hp_kernel) against fwd_pipe_kernel and the oracle.
 
-For each shape: O and LSE2 with the hand-placed forward on and off (fa2_set_path_policy) in one process, max |diff| between them, and
+For each shape: O and LSE2 with the hand-placed forward on and off (_lib.set_path_policy: the per-call fa2_policy) in one process, max |diff| between them, and
 each one's max |O - O_fp32 oracle|.  usage: python tests/hp_check.py
 """
 import os

@@ -10,7 +10,7 @@ no-dropout grid.  Also checked: two backward passes from the same forward are bi
 import pytest
 import torch
 
-from tests.core import assert_dropout_grads_match, generate_test_data, run_case
+from tests.core import assert_dropout_grads_match, generate_test_data, run_case, unpack_keep_mask
 
 CASES = [
     # b, hq, hkv, sq, sk, d, causal, p, dtype
@@ -42,16 +42,6 @@ def test_dropout_backward_is_deterministic():
         assert torch.equal(a, b_)
 
 
-def _unpack_keep_mask(words, b, h, sq, sk):
-    """Dense [B, Hq, Sq, Sk] bool view of the tiled keep mask of include/fa2_amd.h (ABI 6; the
-    ABI-8 slack tile after the last one is not part of the mask)."""
-    nrb, ncw = (sq + 31) // 32, (sk + 31) // 32
-    t = words[: b * h * nrb * ncw * 32].view(b, h, nrb, ncw, 32)  # [.., row tile, key word, row in tile]
-    bits = (t.unsqueeze(-1) >> torch.arange(32, device=words.device, dtype=torch.int32)) & 1
-    dense = bits.permute(0, 1, 2, 4, 3, 5).reshape(b, h, nrb * 32, ncw * 32)
-    return dense[:, :, :sq, :sk].bool()
-
-
 MASK_CASES = [
     # b, hq, hkv, sq, sk, d, causal, p, dtype
     (2, 4, 2, 239, 301, 128, True, 0.17, torch.bfloat16),
@@ -78,7 +68,7 @@ def test_saved_keep_mask_matches_philox_and_regeneration(b, hq, hkv, sq, sk, d, 
     o, lse, scale, seed = _flash_attn_forward(q, k, v, None, None, p, causal, None, seed, dropout_mask=words)
     o_ref, _, _, _ = _flash_attn_forward(q, k, v, None, None, p, causal, None, seed)
     assert torch.equal(o, o_ref)  # writing the mask does not change the forward
-    keep = _unpack_keep_mask(words, b, hq, sq, sk)
+    keep = unpack_keep_mask(words, b, hq, sq, sk)
     want = dropout_keep_mask_torch(seed, p, b, hq, sq, sk, device=q.device)
     vis = torch.ones(sq, sk, dtype=torch.bool, device=q.device)
     if causal:  # bottom-right aligned: key j visible to row i iff j <= i + sk - sq
@@ -104,7 +94,7 @@ def test_keep_mask_layout_unpacks_a_known_pattern():
         dense[0, hh, i, j] = True
         wi = ((hh * nrb + i // 32) * ncw + j // 32) * 32 + i % 32
         words[wi] |= torch.tensor(1 << (j % 32), dtype=torch.int64).to(torch.int32)
-    assert torch.equal(_unpack_keep_mask(words, b, h, sq, sk), dense)
+    assert torch.equal(unpack_keep_mask(words, b, h, sq, sk), dense)
 
 
 def test_keep_mask_allocation_falls_back_on_oom(monkeypatch):
@@ -171,7 +161,7 @@ def test_varlen_dropout_saved_mask(causal):
     seed = 99
     words = torch.full((dropout_mask_words(b, hq, s, s),), -1, dtype=torch.int32, device=q.device)
     o, lse, scale, seed = _flash_attn_forward(q, k, v, mask, None, p, causal, None, seed, dropout_mask=words)
-    keep = _unpack_keep_mask(words, b, hq, s, s)
+    keep = unpack_keep_mask(words, b, hq, s, s)
     cu = 0
     for i, n in enumerate(lens):
         rows = torch.arange(n, device=q.device)

@@ -40,9 +40,30 @@ def _header_struct_fields(name):
     return fields
 
 
-@pytest.mark.parametrize("cname,pystruct", [("fa2_fwd_args", _lib.FwdArgs), ("fa2_bwd_args", _lib.BwdArgs)])
+@pytest.mark.parametrize("cname,pystruct", [("fa2_fwd_args", _lib.FwdArgs), ("fa2_bwd_args", _lib.BwdArgs),
+                                           ("fa2_policy", _lib.Policy)])
 def test_ctypes_struct_matches_header(cname, pystruct):
     assert _header_struct_fields(cname) == [f[0] for f in pystruct._fields_]
+
+
+def test_policy_is_per_call_and_validated():
+    """ABI 9: the kernel-path policy travels with each call (fa2_fwd_ex / fa2_bwd_stages_ex); the
+    library keeps no mutable state between calls (no fa2_set_path_policy).  Bad policies are
+    rejected before any launch."""
+    lib = _lib.load()
+    assert not hasattr(lib, "fa2_set_path_policy")
+    a, b = _lib.FwdArgs(), _lib.BwdArgs()
+    assert lib.fa2_fwd_ex(ctypes.byref(a), ctypes.byref(_lib.Policy(8, 0)), None) == _lib.FA2_E_INVALID
+    assert b"path bits" in lib.fa2_last_error()
+    assert lib.fa2_bwd_stages_ex(ctypes.byref(b), 6, ctypes.byref(_lib.Policy(0, -1)), None) == _lib.FA2_E_INVALID
+    assert b"grid_cap" in lib.fa2_last_error()
+    with pytest.raises(ValueError):
+        _lib.set_path_policy(8, 0)
+    _lib.set_path_policy(_lib.PATH_FWD_HP, 2)
+    try:
+        assert (_lib._policy.disable, _lib._policy.grid_cap) == (_lib.PATH_FWD_HP, 2)
+    finally:
+        _lib.set_path_policy(0, 0)
 
 
 def test_invalid_arguments_are_rejected_without_a_gpu():

@@ -4,7 +4,7 @@ persistent multi-unit paths.
 * Backward: the hand-placed dQ and dK/dV (`dq_hp_kernel`, `dkdv_hp_kernel`) compute the same
   fp32 sums in the same order as `dq_kernel` / `dkdv_kernel` (same math as the reference's loops,
   /root/reference/src/backward/compute_dq.py:38-78, compute_dkdv.py:42-112), so dQ, dK, dV must be
-  BITWISE equal with the hand-placed paths on and off (fa2_set_path_policy, ABI 7).
+  BITWISE equal with the hand-placed paths on and off (the per-call fa2_policy, ABI 9).
 * Forward: `fwd_hp_kernel` and `fwd_pipe_kernel` order the softmax differently (defer-max
   thresholds, tile phases): both within the reference's tolerance of the oracle, LSE2 within 1e-3.
 * Persistence: one workgroup per CU walks several work units when the grid is capped
@@ -16,7 +16,8 @@ persistent multi-unit paths.
 import pytest
 import torch
 
-from tests.core import assert_dropout_grads_match, generate_attention_mask, generate_test_data
+from tests.core import (assert_dropout_dv_vs_oracle, assert_dropout_grads_match, generate_attention_mask,
+                        generate_test_data)
 
 BWD_CASES = [
     # b, hq, hkv, sq, sk, causal, dtype
@@ -138,6 +139,7 @@ def test_dropout_hand_placed_dq_multi_unit(causal, cap, policy):
     regen = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=None)
     policy.set_path_policy(0, 0)
     assert_dropout_grads_match(hp[:3], regen[:3])
+    assert_dropout_dv_vs_oracle(hp[2], regen[2], q, k, v, do, words, p, causal)
 
 
 DROP_CASES = [
@@ -170,3 +172,4 @@ def test_dropout_hand_placed_dkdv(b, hq, hkv, sq, sk, causal, p, dtype, cap, pol
     gen = _flash_attn_backward(do, q, k, v, None, None, o, lse, p, causal, scale, seed, dropout_mask=words)
     policy.set_path_policy(0, 0)
     assert_dropout_grads_match(hp[:3], gen[:3])
+    assert_dropout_dv_vs_oracle(hp[2], gen[2], q, k, v, do, words, p, causal)
