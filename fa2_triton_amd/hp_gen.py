@@ -322,6 +322,11 @@ N_NEXT = 12 + 16  # vector-memory ops of the next-unit requests (3 tiles x 4 pie
 
 LEADK = 3  # K fragments in flight ahead of their MFMAs
 LEADV = 3
+# round 6 experiment, off by default (FA2_HPGEN_ABL=fw_sd4 / fw_sd6): the last FW_SD PV MFMAs of a
+# class A / B period run at the start of the next period, to cover the LDS latency of its first K
+# fragments.  Same-box A/B (profiles/r06d_ab_fwd_schedules_*.txt): 1 % slower -- the apparent
+# start-of-period latency in the stamp build was the stamp's own s_memtime wait
+FW_SD = 4 if "fw_sd4" in ABL else (6 if "fw_sd6" in ABL else 0)
 
 
 def elem_order():
@@ -586,15 +591,47 @@ class FwdGen:
                 for j in range(1, 16):
                     e.valu(f"v_mov_b32 {INIT(rb, j)}, {INIT(rb, 0)}", INIT(rb, j), [INIT(rb, 0)])
 
-    def vote_and_rescale(self, st, tag):
-        """One wave vote: any row of either block whose max outgrew its threshold -> rescale."""
+    def vote_and_rescale(self, st, tag, sd=0):
+        """One wave vote: any row of either block whose max outgrew its threshold -> rescale.
+        sd > 0: the period's last sd PV MFMAs are deferred to the next period; a rescale runs
+        them first (O must hold all of P(i) before it is scaled) and zeroes their P operands, so
+        the deferred copies at the next period's start add zeros."""
         e = self.e
         e.valu(f"v_cmp_gt_f32_e64 {SVOTE}, {MX[0]}, {THR[0]}", None, [MX[0], THR[0]])
         e.valu(f"v_cmp_gt_f32_e64 {SVOTE2}, {MX[1]}, {THR[1]}", None, [MX[1], THR[1]])
         e.salu(f"s_or_b64 {SVOTE}, {SVOTE}, {SVOTE2}")
         e.raw(f"s_cbranch_scc0 .Lhp%=_{tag}_nr")
+        if sd:
+            self.deferred_pv(sd)
+            e.drain_mfma()
         self.rescale(st)
+        if sd:
+            self.zero_deferred_p(sd)
         e.label(f".Lhp%=_{tag}_nr")
+
+    def deferred_pv(self, sd, only=None):
+        """The last sd PV MFMAs of a period (O^T[rb][dt] += V^T(m) P(rb, kk = 3)), run at the start of
+        the next one: their operands (V^T fragments in ring slots m % 4, packs PF(rb, 3)) stay in
+        registers across the barrier.  only = i: just the i-th of them."""
+        e = self.e
+        ny = 8 * self.ndt
+        for n, g in enumerate(range(ny - sd, ny)):
+            if only is not None and n != only:
+                continue
+            m, rb = g >> 1, g & 1
+            kk, dt = m // self.ndt, m % self.ndt
+            e.mfma(self.mop, self.o(rb, dt), VR(m % 4), PF(rb, kk), self.o(rb, dt))
+
+    def zero_deferred_p(self, sd):
+        """Zero the P packs the deferred MFMAs read (and, for a unit's first period, make their
+        V^T ring slots finite: uninitialised accumulation registers could hold NaN patterns)."""
+        e = self.e
+        ny = 8 * self.ndt
+        kks = sorted({((g >> 1) // self.ndt) for g in range(ny - sd, ny)})
+        for rb in range(2):
+            for kk in kks:
+                for j in range(4):
+                    e.valu(f"v_mov_b32 {PF(rb, kk, j)}, 0", PF(rb, kk, j))
 
     # -- s_memtime stamps (FA2_HP_STAMPS development builds only) ---------------------------------
     # per period: s[96:97] = its start (after the previous barrier), s[92:93] = the start of phase
@@ -747,6 +784,22 @@ class FwdGen:
         qk = cls in ("A", "B")
         masked = cls == "B"
         E = elem_order()
+        # development timing ablations of the steady-state (class A) period: FA2_HPGEN_ABL=fw_*
+        # (wrong outputs; cycles only, read with the stamp build)
+        drops = {"fw_nodma": r"^buffer_load|^s_add_u32 m0", "fw_noexp": r"^v_exp",
+                 "fw_novalu": r"^v_(?!mfma)", "fw_nolds": r"^ds_read", "fw_nosalu": r"^s_(?!waitcnt|barrier|cbranch|nop|branch)"}
+        pat = "|".join(v for k, v in drops.items() if k in ABL) if cls == "A" else ""
+        e.drop = re.compile(pat) if pat else None
+        if qk and self.dt == 128 and "fw_r5" not in ABL:
+            # round 6: the balanced period (period_xy_bal)
+            self.period_xy_bal(par, masked, tag, final, E)
+            e.drop = None
+            self.period_end(final)
+            return
+        if self.dt == 128 and FW_SD and "fw_r5" not in ABL:
+            # class C follows a class A / B period (or a unit's prologue, which zeroed their
+            # operands): its deferred PV MFMAs first
+            self.deferred_pv(FW_SD)
         if final:
             dma = self.next_unit_items(par)
         else:
@@ -793,12 +846,6 @@ class FwdGen:
             d = S(nxt, rb, t)
             e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * self.ks + ks}]", self.chain0(rb) if ks == 0 else d)
 
-        # development timing ablations of the steady-state (class A) period: FA2_HPGEN_ABL=fw_*
-        # (wrong outputs; cycles only, read with the stamp build)
-        drops = {"fw_nodma": r"^buffer_load|^s_add_u32 m0", "fw_noexp": r"^v_exp",
-                 "fw_novalu": r"^v_(?!mfma)", "fw_nolds": r"^ds_read", "fw_nosalu": r"^s_(?!waitcnt|barrier|cbranch|nop|branch)"}
-        pat = "|".join(v for k, v in drops.items() if k in ABL) if cls == "A" else ""
-        e.drop = re.compile(pat) if pat else None
         if qk:
             for m in range(LEADK):
                 self.k_read(kbuf, m)
@@ -857,6 +904,149 @@ class FwdGen:
         e.drop = None
         self.period_end(final)
 
+    def row_max_finish_items(self):
+        """row_max_finish as a list of emit functions (scheduled into the last PV gaps)."""
+        e = self.e
+        out = []
+        for rb in range(2):
+            out.append(lambda rb=rb: e.valu(f"v_max_f32 {MX[rb]}, {MAH[rb][0]}, {MAH[rb][1]}", MX[rb], MAH[rb]))
+            out.append(lambda rb=rb: e.valu(f"v_mov_b32 {TMP[rb]}, {MX[rb]}", TMP[rb], [MX[rb]]))
+        for rb in range(2):
+            out.append(lambda rb=rb: e.valu(f"v_permlane32_swap_b32 {MX[rb]}, {TMP[rb]}", [MX[rb], TMP[rb]],
+                                            [MX[rb], TMP[rb]], kind="perm"))
+        for rb in range(2):
+            out.append(lambda rb=rb: e.valu(f"v_max_f32 {MX[rb]}, {MX[rb]}, {TMP[rb]}", MX[rb], [MX[rb], TMP[rb]]))
+        if self.exact:
+            for rb in range(2):
+                out.append(lambda rb=rb: e.valu(f"v_fma_f32 {MX[rb]}, {MX[rb]}, %[uz], {INIT(rb, 0)}", MX[rb],
+                                                [MX[rb], INIT(rb, 0)]))
+        return out
+
+    def period_xy_bal(self, par, masked, tag, final, E):
+        """Class A / B period at D = 128 with the fillers balanced over both phases (round 6).
+
+        The round-5 schedule put 56 of the 64 exponentials of tile i into phase X (two or three per
+        MFMA gap, where one v_exp per gap hides) and left phase Y with every row sum and the whole
+        mask / row max / exponent-argument pass of tile i+1 -- more than its 32 gaps hold, so ~60
+        instructions ran after its last MFMA (s_memtime stamps, profiles/r06a_fwd_stamps_ablations.jsonl:
+        X 1369 and Y 1400 cycles per period against 1024 of MFMAs).  Here:
+          X: K fragment reads (issued first in the period, before the descriptor updates), the
+             exponentials of E[0:40] (kk = 0, 1 and half of kk = 2), the packs of kk = 0 and 1, the row
+             sums of kk = 0, the LDS-DMA pieces, and -- once the chains S(i+1)[rb][t = 0] are complete
+             (MFMAs 14, 15) -- the t = 0 half of the mask / row max / exponent arguments of tile i+1;
+          Y: the remaining 24 exponentials, the kk = 2, 3 packs, the other row sums, the t = 1 half of
+             the next tile's pass, and the row-max finish in its last gaps (the vote after the last
+             MFMA).
+        Every cross-stream dependence is a release after the producer's deadline (a stream orders
+        only itself)."""
+        e = self.e
+        cur, nxt = par, 1 - par
+        kbuf, vbuf = 1 - par, par
+        nk, nx, nv = 2 * self.ks, 4 * self.ks, 4 * self.ndt
+        sd = FW_SD
+        ny = 2 * nv - sd  # this period's PV MFMAs; the last sd run at the next period's start
+        # the first K fragments first: their LDS latency runs under the scalar updates below
+        for m in range(LEADK):
+            self.k_read(kbuf, m)
+        if final:
+            dma = self.next_unit_items(par)
+        else:
+            self.descriptors()
+            dma = self.dma_stream(par)
+        if masked:
+            for rb in range(2):
+                e.valu(f"v_subrev_u32 {REL[rb]}, {SN1}, %[rel{rb}]", REL[rb], [])
+
+        def zprep(add, t, rb, release, deadline):
+            st_ = f"mx{t}{rb}"
+            if masked:
+                for i in range(16):
+                    add(st_, 8, release, deadline, lambda rb=rb, t=t, i=i: self.mask_elem(nxt, rb, t, i))
+            for op in self.max_ops_z(nxt, rb, t):
+                if op[0] == "max":
+                    add(st_, 4, release, deadline, lambda op=op: e.valu(op[1], op[2], op[3]))
+                else:
+                    add(st_, 4, release, deadline, lambda op=op: self.fma_z(nxt, *op[1:]))
+
+        # ---------------- phase X ----------------
+        # gap indices of phase X count from its first QK^T MFMA (the sd deferred PV MFMAs before it
+        # are gaps -sd .. -1); GapScheduler positions are those + sd
+        n_x = 40
+        x_dl = {n: (n * 28) // n_x for n in range(n_x)}
+        gx = GapScheduler(nx + sd)
+
+        def gxa(stream, cost, rel, dl, f):
+            gx.add(stream, cost, rel + sd if rel >= 0 else rel, dl + sd, f)
+        for m in range(nk):
+            if m + LEADK < nk:
+                gxa("k", 4, 2 * m, 2 * m, lambda m=m: self.k_read(kbuf, m + LEADK))
+        # (released one gap before the deadline: about one exponential per gap instead of a burst of
+        # three, MI355X_MICROARCH.md filler rule "at most one v_exp per MFMA gap")
+        for n in range(n_x):
+            gxa("exp", 8, x_dl[n] - 1, x_dl[n], lambda el=E[n]: self.exp(cur, el))
+        for n, f in enumerate(dma):
+            gxa("dma", f[0], -1, min(nx - 1, (4 * n + 3) * nx // 32), f[1])
+        for kk in (0, 1):
+            for rb in range(2):
+                for j in range(4):
+                    idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
+                    gxa(f"cvt{kk}", 4, max(x_dl[i] for i in idx) + 1, nx - 1,
+                        lambda c=(rb, kk, j): self.cvt(cur, *c))
+        for n in range(16):
+            gxa(f"add{n % 2}", 4, x_dl[n] + 1, nx - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
+        for m in range(LEADV):
+            for h in range(2):
+                gxa("vr", 4, max(0, nx - 12), nx - 1, lambda m=m, h=h: self.v_read(vbuf, m, h))
+        # S(i+1)[rb][0] is complete after MFMA 14 + rb
+        for rb in range(2):
+            zprep(gxa, 0, rb, 17 + rb, nx - 1)
+
+        def x_mfma(g):
+            if g < sd:  # the previous period's deferred PV MFMAs (zeros after a unit start / rescale)
+                self.deferred_pv(sd, only=g)
+                return
+            g -= sd
+            m, rb = g >> 1, g & 1
+            t, ks = m // self.ks, m % self.ks
+            d = S(nxt, rb, t)
+            e.mfma(self.mop, d, KR(m % 4), f"%[q{rb * self.ks + ks}]", self.chain0(rb) if ks == 0 else d)
+
+        # (before the first MFMA the wave waits for its first K fragment anyway: room for fillers)
+        gx.run(x_mfma, pre_budget=64)
+        if self.stamp:
+            e.raw("s_memtime s[92:93]")
+        # ---------------- phase Y ----------------
+        gy = GapScheduler(ny)
+        for m in range(nv):
+            if m + LEADV < nv:
+                for h in range(2):
+                    gy.add("v", 4, 2 * m, 2 * m + 1, lambda m=m, h=h: self.v_read(vbuf, m + LEADV, h))
+        y_dl = {n: ((n - n_x) * 20) // (64 - n_x) for n in range(n_x, 64)}
+        for n in range(n_x, 64):
+            gy.add("exp", 8, y_dl[n] - 1, y_dl[n], lambda el=E[n]: self.exp(cur, el))
+        # packs of P(kk) before the first PV MFMA reading them (MFMA 8 kk; margin for VALU -> MFMA)
+        for kk in (2, 3):
+            for rb in range(2):
+                for j in range(4):
+                    idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
+                    rel = max([y_dl[i] for i in idx if i in y_dl] + [-2]) + 1
+                    gy.add(f"cvt{kk}", 4, rel, (13, 21)[kk - 2], lambda c=(rb, kk, j): self.cvt(cur, *c))
+        for n in range(16, 64):
+            rel = y_dl[n] + 1 if n in y_dl else -1
+            gy.add(f"add{n % 2}", 4, rel, ny - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
+        for rb in range(2):
+            zprep(gy.add, 1, rb, -1, ny - 4)
+        for f in self.row_max_finish_items():
+            gy.add("rmf", 4, ny - 3, ny - 1, f)
+
+        def y_mfma(g):
+            m, rb = g >> 1, g & 1
+            kk, dt = m // self.ndt, m % self.ndt
+            e.mfma(self.mop, self.o(rb, dt), VR(m % 4), PF(rb, kk), self.o(rb, dt))
+
+        gy.run(y_mfma, pre_budget=0)
+        self.vote_and_rescale(nxt, tag, sd)
+
     def dma_stream(self, par):
         """The period's 8 LDS-DMA pieces as (cost, emit) items; each item issues its piece and
         already points m0 at the next one, so no piece waits on its own m0 write."""
@@ -911,6 +1101,13 @@ class FwdGen:
             for dt in range(self.ndt):
                 for i in range(16):
                     e.valu(f"v_accvgpr_write_b32 {self.o(rb, dt, i)}, 0", self.o(rb, dt, i), kind="accw")
+        if self.dt == 128 and FW_SD and "fw_r5" not in ABL:
+            # the first period's deferred PV MFMAs add V^T x 0: zero packs, finite V^T ring slots
+            self.zero_deferred_p(FW_SD)
+            ny = 8 * self.ndt
+            for slot in sorted({((g >> 1) % 4) for g in range(ny - FW_SD, ny)}):
+                for r in _regs(VR(slot)):
+                    e.valu(f"v_accvgpr_write_b32 {r}, 0", r, kind="accw")
         # DMA cursors: period i requests K(i + 2) and V(i + 1)
         e.salu(f"s_mov_b32 {SKP[0]}, %[klo]")
         e.salu(f"s_mov_b32 {SKP[1]}, %[khi]")
