@@ -1687,18 +1687,41 @@ class DkdvGen:
         masked = cls == "B"
         if masked and self.causal:
             self.mask_bases()
-        g = GapScheduler(64 if live else 24, lds_cap=None if "dk_nocap" in ABL else 3)
+        # the MFMAs of the step (indices of `mfma` below): a live step all 64; a dead step (no key of
+        # the wave visible) only what a neighbour needs (round 6; round 5 ran the straddled eight and
+        # S(i+1) in every dead step: 3.9 % more MFMAs than the algorithm per launch) --
+        #   D  (the head's first dead step, also its last): the straddled MFMAs that finish the last
+        #      live step's dK, and S(i+1) for the next head's first step;
+        #   Ds (first dead step, more follow): the straddled MFMAs only;
+        #   E  (neither first nor last): none;
+        #   F  (the head's last dead step after others): S(i+1) only
+        mf = list(range(64)) if live else {"D": list(range(24)), "Ds": list(range(8)), "E": [],
+                                           "F": list(range(8, 24))}[cls]
+        if "dk_r5" in ABL and not live:  # A/B reference: round 5's dead steps (24 MFMAs each)
+            mf = list(range(24))
+        pos = {m: n for n, m in enumerate(mf)}
+        last = max(len(mf) - 1, -1)
+        g = GapScheduler(len(mf), lds_cap=None if "dk_nocap" in ABL else 3)
         # Q(i+1) row fragments ks -> ring slot ks % 4 (after the slot's previous occupant's last
-        # MFMA: the straddled MFMAs 2 dt + kb, then S MFMAs 8 + 2 ks + kb)
-        for ks in range(8):
-            rel = 2 * ks + 1
-            g.add("row", 4, rel, rel + 4, lambda ks=ks: self.row_read(nxt, False, ks), lds=2)
+        # MFMA: the straddled MFMAs 2 dt + kb, then S MFMAs 8 + 2 ks + kb); none without S(i+1)
+        if 8 in pos:
+            for ks in range(8):
+                if 0 in pos:
+                    rel, dl = 2 * ks + 1, 2 * ks + 5
+                else:
+                    # F: no straddled MFMA reads the slots (the step before was Ds or E), so
+                    # fragments 0-3 go at once; fragment ks >= 4 reuses slot ks % 4 only after
+                    # both S MFMAs of fragment ks - 4 have read it
+                    rel = -1 if ks < 4 else pos[8 + 2 * (ks - 4) + 1] + 1
+                    dl = max(rel, pos[8 + 2 * ks] - 3)
+                g.add("row", 4, rel, dl, lambda ks=ks: self.row_read(nxt, False, ks), lds=2)
         items = [it for nb, t in reqs for it in self.dma_items(nb, t)]
         for n, (c, f) in enumerate(items):
             if pair:
-                dl = min(20 + 3 * n, 62) if live else min(6 + n, 23)
+                dl = min(20 + 3 * n, 62) if live else min(6 + n, last)
             else:
                 dl = (20 if early and live else 42 if live else 14) + 3 * n
+                dl = dl if live else min(dl, last)
             g.add("dma", c, 0 if early or not live else 2, dl, f)
         if live:
             # dO(i) row fragments ks (slot ks % 4, after the S MFMAs 2 ks + 17), dP at 24 + 2 ks
@@ -1802,13 +1825,14 @@ class DkdvGen:
                         g.add(f"ds{kb}", 4, 43, dl + 1,
                               lambda kb=kb, sp=sp, j=j: self.cvt(DDSP(kb, sp, j), DDP(kb, 8 * sp + 2 * j), DDP(kb, 8 * sp + 2 * j + 1)))
         else:
-            # no dS of this step: the next step's straddled MFMAs add zeros
+            # no dS of this step: the next step's straddled MFMAs add zeros (after this step's
+            # straddled MFMAs, which read the packs)
             for kb in range(2):
                 for j in range(4):
                     r = DDSP(kb, 1, j)
-                    g.add("zero", 4, 7 + kb, 20, lambda r=r: e.valu(f"v_mov_b32 {r}, 0", r))
+                    g.add("zero", 4, (7 + kb) if 0 in pos else -1, min(20, last), lambda r=r: e.valu(f"v_mov_b32 {r}, 0", r))
             for g4 in (0, 1):  # the next step's LSE2 of half sp = 0
-                g.add("lse", 4, -1, 20, lambda g4=g4: self.init_read(nxt, 0, 0, g4), lds=2)
+                g.add("lse", 4, -1, min(20, last), lambda g4=g4: self.init_read(nxt, 0, 0, g4), lds=2)
 
         if "dk_novalu" in ABL:
             g.items = [it for it in g.items if not it["stream"].startswith(("exp", "ds"))]
@@ -1828,7 +1852,8 @@ class DkdvGen:
         pat = "|".join(v for k, v in drops.items() if k in ABL)
         e.drop = re.compile(pat) if pat else None
 
-        def mfma(m):
+        def mfma(n):
+            m = mf[n]
             if m < 8:
                 self.mf_dk_tail(m)
             elif m < 24:
@@ -1950,11 +1975,21 @@ class DkdvGen:
             e.raw(f"s_cbranch_scc1 .Lhp%=_A{ph}")
             e.raw(f"s_cmp_lt_u32 {D_IDX}, %[c012]")
             e.raw(f"s_cbranch_scc1 .Lhp%=_B{ph}")
+            # dead steps: D / Ds at IDX == c012 (with / without more after it), E between, F last
+            e.salu(f"s_add_u32 {D_T}, {D_IDX}, 1")
+            e.raw(f"s_cmp_eq_u32 {D_IDX}, %[c012]")
+            e.raw(f"s_cbranch_scc0 .Lhp%=_nd{ph}")
+            e.raw(f"s_cmp_lt_u32 {D_T}, %[nmt]")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_Ds{ph}")
             e.raw(f"s_branch .Lhp%=_D{ph}")
+            e.label(f".Lhp%=_nd{ph}")
+            e.raw(f"s_cmp_lt_u32 {D_T}, %[nmt]")
+            e.raw(f"s_cbranch_scc1 .Lhp%=_E{ph}")
+            e.raw(f"s_branch .Lhp%=_F{ph}")
         snaps = []
         for ph in range(self.L.ph):
             ends = []
-            for cls in ("A", "B", "D"):
+            for cls in ("A", "B", "D", "Ds", "E", "F"):
                 nph = (ph + 1) % self.L.ph
                 e.label(f".Lhp%=_{cls}{ph}")
                 # half barriers: an odd step follows any of the previous phase's bodies with no
@@ -1965,7 +2000,7 @@ class DkdvGen:
                     e.reset()
                 self.step(ph, cls, f"{cls.lower()}{ph}")
                 if self.L.halfbar and not ph & 1:
-                    if cls == "D":  # (rare: a head's last steps; its S MFMAs end the body)
+                    if cls not in ("A", "B"):  # (rare: a head's dead steps)
                         e.close_windows()
                     ends.append(e.snapshot())
                 # next step: within the head, else the next head's first (IDX 0, CM = mlast)

@@ -72,6 +72,24 @@ def test_hand_placed_backward_bitwise_equals_general(b, hq, hkv, sq, sk, causal,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,dtype", [c for c in BWD_CASES if c[1] > c[2]],
+                         ids=lambda x: str(x).replace("torch.", ""))
+def test_hand_placed_backward_whole_group_per_block(b, hq, hkv, sq, sk, causal, dtype, policy, monkeypatch):
+    """As above with the dK/dV q-head split off (FA2_DKV_SPLIT=0): one workgroup sums the whole GQA
+    group, so a key block's step sequence runs several heads back to back and a head's dead causal
+    steps (the classes D / Ds / E / F of hp_gen.DkdvGen) hand over to the next head's first step,
+    whose S the last dead step computes (the small grids here would otherwise split the group)."""
+    monkeypatch.setenv("FA2_DKV_SPLIT", "0")
+    q, k, v, do = generate_test_data(b, hq, hkv, sq, sk, 128, dtype)
+    hp = _fwd_bwd(q, k, v, do, causal, policy=policy, disable=policy.PATH_FWD_HP)
+    gen = _fwd_bwd(q, k, v, do, causal, policy=policy,
+                   disable=policy.PATH_FWD_HP | policy.PATH_DQ_HP | policy.PATH_DKDV_HP)
+    for name, a, c in zip(("out", "dq", "dk", "dv"), hp, gen):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,dtype", BWD_CASES[:6], ids=lambda x: str(x).replace("torch.", ""))
 def test_hand_placed_forward_matches_pipelined(b, hq, hkv, sq, sk, causal, dtype, policy):
     from fa2_triton_amd.forward import _flash_attn_forward
