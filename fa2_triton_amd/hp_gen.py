@@ -495,6 +495,13 @@ class FwdGen:
         l = LSUM[rb][c]
         self.e.valu(f"v_add_f32 {l}, {l}, {r}", l, [l, r])
 
+    def add_pk(self, st, el):
+        """LSUM[rb][0:1] += the element pair (i, i + 1) (i even), one v_pk_add_f32."""
+        kk, rb, t, i = el
+        r = f"v[{S(st, rb, t, i)[1:]}:{S(st, rb, t, i + 1)[1:]}]"
+        l = f"v[{LSUM[rb][0][1:]}:{LSUM[rb][1][1:]}]"
+        self.e.valu(f"v_pk_add_f32 {l}, {l}, {r}", l, [l, r])
+
     def mask_elem(self, st, rb, t, i):
         """z = key offset o < rel[rb] ? z : -inf  (o = 32 t + (i & 3) + 8 (i >> 2))."""
         o = 32 * t + (i & 3) + 8 * (i >> 2)
@@ -992,8 +999,12 @@ class FwdGen:
                     idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
                     gxa(f"cvt{kk}", 4, max(x_dl[i] for i in idx) + 1, nx - 1,
                         lambda c=(rb, kk, j): self.cvt(cur, *c))
-        for n in range(16):
-            gxa(f"add{n % 2}", 4, x_dl[n] + 1, nx - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
+        if "fw_pk" in ABL:  # (A/B: row sums of element pairs by v_pk_add_f32, same partial sums)
+            for n in range(0, 16, 2):
+                gxa("add", 8, max(x_dl[n], x_dl[n + 1]) + 1, nx - 1, lambda el=E[n]: self.add_pk(cur, el))
+        else:
+            for n in range(16):
+                gxa(f"add{n % 2}", 4, x_dl[n] + 1, nx - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
         for m in range(LEADV):
             for h in range(2):
                 gxa("vr", 4, max(0, nx - 12), nx - 1, lambda m=m, h=h: self.v_read(vbuf, m, h))
@@ -1031,9 +1042,14 @@ class FwdGen:
                     idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
                     rel = max([y_dl[i] for i in idx if i in y_dl] + [-2]) + 1
                     gy.add(f"cvt{kk}", 4, rel, (13, 21)[kk - 2], lambda c=(rb, kk, j): self.cvt(cur, *c))
-        for n in range(16, 64):
-            rel = y_dl[n] + 1 if n in y_dl else -1
-            gy.add(f"add{n % 2}", 4, rel, ny - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
+        if "fw_pk" in ABL:
+            for n in range(16, 64, 2):
+                rel = max(y_dl.get(n, -2), y_dl.get(n + 1, -2)) + 1
+                gy.add("add", 8, rel, ny - 1, lambda el=E[n]: self.add_pk(cur, el))
+        else:
+            for n in range(16, 64):
+                rel = y_dl[n] + 1 if n in y_dl else -1
+                gy.add(f"add{n % 2}", 4, rel, ny - 1, lambda el=E[n], c=n % 2: self.add(cur, el, c))
         for rb in range(2):
             zprep(gy.add, 1, rb, -1, ny - 4)
         for f in self.row_max_finish_items():
@@ -1820,6 +1836,12 @@ class DkdvGen:
                     dl = 52 if sp == 0 else 61
                     for i in range(8 * sp, 8 * sp + 8):
                         a_, b_ = DS(st, kb, i), DDP(kb, i)
+                        if "dk_pk" in ABL:  # (A/B: dS of element pairs by v_pk_mul_f32)
+                            if not i & 1:
+                                a2, b2 = rng("v", int(a_[1:]), 2), rng("v", int(b_[1:]), 2)
+                                g.add(f"ds{kb}", 8, 43, dl,
+                                      lambda a2=a2, b2=b2: e.valu(f"v_pk_mul_f32 {b2}, {a2}, {b2}", b2, [a2, b2]))
+                            continue
                         g.add(f"ds{kb}", 4, 43, dl, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
                     for j in range(4):
                         g.add(f"ds{kb}", 4, 43, dl + 1,
@@ -2121,6 +2143,15 @@ def QTR(n, half=None):
 
 
 QREL = ["v176", "v177"]
+# round 6 (no dropout): -delta of the lane's row in all 16 registers of a block per row block: the
+# C operand of the first dP MFMA of both key halves, so the chain yields dP - delta and dS is one
+# multiply (as dkdv_hp; dq_kernel seeds its chain the same way, the two stay bitwise equal)
+
+
+def QNDEL(rb):
+    return rng("v", 178 + 16 * rb, 16)
+
+
 DQ_NVGPR = 178
 # dropout (the forward's saved keep words, one 32-key word per row): the words of the current and
 # the next tile, per (rb, key half h); per-stream temporaries; the lane's word offsets (cursor)
@@ -2160,6 +2191,7 @@ class DqGen:
 
     def __init__(self, bf16, causal, dropout=False):
         self.bf16, self.causal, self.dropout = bf16, causal, dropout
+        self.seed = not dropout and "dq_r5" not in ABL  # dP chains seeded with -delta (QNDEL)
         self.mop = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvtop = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.e = Emitter()
@@ -2286,10 +2318,16 @@ class DqGen:
                                   lambda t_=t_, b_=b_: e.valu(f"v_and_b32 {b_}, {t_}, {b_}", b_, [t_, b_]))
                             g.add(st, 4, rel1, 58 + 16 * h,
                                   lambda b_=b_, rb=rb: e.valu(f"v_fma_f32 {b_}, {b_}, %[dsc], -%[del{rb}]", b_, [b_]))
-                        else:
+                        elif not self.seed:  # (A/B reference, FA2_HPGEN_ABL=dq_r5)
                             g.add(st, 4, rel1, 58 + 16 * h,
                                   lambda b_=b_, rb=rb: e.valu(f"v_sub_f32 {b_}, {b_}, %[del{rb}]", b_, [b_]))
-                        g.add(st, 4, rel1, 60 + 16 * h, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
+                        if "dq_pk" in ABL and self.seed:  # (A/B: dS of element pairs by v_pk_mul_f32)
+                            if not i & 1:
+                                a2, b2 = rng("v", int(a_[1:]), 2), rng("v", int(b_[1:]), 2)
+                                g.add(st, 8, rel1, 60 + 16 * h,
+                                      lambda a2=a2, b2=b2: e.valu(f"v_pk_mul_f32 {b2}, {a2}, {b2}", b2, [a2, b2]))
+                        else:
+                            g.add(st, 4, rel1, 60 + 16 * h, lambda a_=a_, b_=b_: e.valu(f"v_mul_f32 {b_}, {a_}, {b_}", b_, [a_, b_]))
                         if i & 1:
                             kk, j = 2 * h + (i >> 3), (i & 7) >> 1
                             g.add(st, 4, rel1, 62 + 16 * h,
@@ -2306,7 +2344,8 @@ class DqGen:
                     x = gi - 32
                     h, ks, rb = x >> 4, (x >> 1) & 7, x & 1
                     d = QDP(rb, h)
-                    e.mfma(self.mop, d, QVR(8 * h + ks), f"%[o{rb * 8 + ks}]", "0" if ks == 0 else d)
+                    c0 = QNDEL(rb) if self.seed else "0"
+                    e.mfma(self.mop, d, QVR(8 * h + ks), f"%[o{rb * 8 + ks}]", c0 if ks == 0 else d)
                 else:
                     f_, rb = (gi - 64) >> 1, gi & 1
                     kk, dt = f_ >> 2, f_ & 3
@@ -2348,6 +2387,10 @@ class DqGen:
         e.salu(f"s_mov_b32 {SM0}, m0")
         for r in range(128):
             e.valu(f"v_accvgpr_write_b32 a{r}, 0", f"a{r}", kind="accw")
+        if self.seed:  # -delta blocks (QNDEL): the dP chains' initial accumulators
+            for rb in range(2):
+                for r in _regs(QNDEL(rb)):
+                    e.valu(f"v_sub_f32 {r}, 0, %[del{rb}]", r)
         # DMA cursors: period i requests K(i + 1), V(i + 1); the final period's requests are the
         # next unit's K(0), V(0) (cursors switched to its slices), into the buffer it starts on
         e.salu(f"s_mov_b32 {SKP[0]}, %[klo]")
@@ -2475,7 +2518,7 @@ def gen_dq_function(bf16, causal, dropout=False):
     g = DqGen(bf16, causal, dropout)
     lines = g.build()
     name = f"dq_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'_drop' if dropout else ''}"
-    nv = DQ_NVGPR_DROP if dropout else DQ_NVGPR
+    nv = DQ_NVGPR_DROP if dropout else DQ_NVGPR + 32
     clob = [f'"v{i}"' for i in range(nv)] + [f'"a{i}"' for i in range(128)] + \
            [f'"s{i}"' for i in _sgprs_used(lines)] + ['"vcc"', '"scc"', '"memory"']
     qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(16))

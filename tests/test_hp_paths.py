@@ -1,10 +1,12 @@
 """The hand-placed D = 128 kernels against the general kernels of the same launch, and their
 persistent multi-unit paths.
 
-* Backward: the hand-placed dQ and dK/dV (`dq_hp_kernel`, `dkdv_hp_kernel`) compute the same
-  fp32 sums in the same order as `dq_kernel` / `dkdv_kernel` (same math as the reference's loops,
-  /root/reference/src/backward/compute_dq.py:38-78, compute_dkdv.py:42-112), so dQ, dK, dV must be
-  BITWISE equal with the hand-placed paths on and off (the per-call fa2_policy, ABI 9).
+* Backward: the hand-placed dK/dV (`dkdv_hp_kernel`) computes the same fp32 sums in the same order
+  as `dkdv_kernel` (same math as the reference's loop, /root/reference/src/backward/
+  compute_dkdv.py:42-112), so dK and dV must be BITWISE equal with the hand-placed paths on and off
+  (the per-call fa2_policy, ABI 9).  The hand-placed dQ (round 6) starts its dP chain from -delta
+  (dS = P acc, one multiply; `dq_kernel` subtracts delta after the chain, as the reference's
+  compute_dq.py:70-76), so dQ may differ by the rounding of dP - delta (assert_hp_vs_general).
 * Forward: `fwd_hp_kernel` and `fwd_pipe_kernel` order the softmax differently (defer-max
   thresholds, tile phases): both within the reference's tolerance of the oracle, LSE2 within 1e-3.
 * Persistence: one workgroup per CU walks several work units when the grid is capped
@@ -45,6 +47,23 @@ def policy():
     L.set_path_policy(0, 0)
 
 
+def assert_hp_vs_general(hp, gen):
+    """out, dK, dV bitwise; dQ within one ulp of the dtype per element (the -delta seed)."""
+    for name, a, c in zip(("out", "dq", "dk", "dv"), hp, gen):
+        assert torch.isfinite(a).all(), name
+        if name != "dq":
+            assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+            continue
+        # the seed moves dP - delta by an fp32 rounding, which can flip the rounding of a dS element
+        # packed to the dtype (2^-8 of |dS|) and so move a dQ element by that term's share of the
+        # sum, independent of the element's own size: two ulps of |x| (a binade edge) plus a
+        # quarter ulp of the largest |dQ|; a wrong dS element moves dQ by far more
+        ulp = 2.0 ** -7 if a.dtype == torch.bfloat16 else 2.0 ** -10
+        err = (a.float() - c.float()).abs()
+        tol = 2 * ulp * c.float().abs() + 0.25 * ulp * c.float().abs().max().item() + 1e-6
+        assert bool((err <= tol).all()), f"dq: {int((err > tol).sum())} elements over one ulp, max |diff| {err.max().item():.3e}"
+
+
 def _fwd_bwd(q, k, v, do, causal, mask=None, dropout_p=0.0, seed=None, policy=None, disable=0, cap=0):
     from fa2_triton_amd import flash_attn_func
 
@@ -66,9 +85,7 @@ def test_hand_placed_backward_bitwise_equals_general(b, hq, hkv, sq, sk, causal,
     hp = _fwd_bwd(q, k, v, do, causal, policy=policy, disable=policy.PATH_FWD_HP)
     gen = _fwd_bwd(q, k, v, do, causal, policy=policy,
                    disable=policy.PATH_FWD_HP | policy.PATH_DQ_HP | policy.PATH_DKDV_HP)
-    for name, a, c in zip(("out", "dq", "dk", "dv"), hp, gen):
-        assert torch.isfinite(a).all(), name
-        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+    assert_hp_vs_general(hp, gen)
 
 
 @pytest.mark.gpu
@@ -84,9 +101,7 @@ def test_hand_placed_backward_whole_group_per_block(b, hq, hkv, sq, sk, causal, 
     hp = _fwd_bwd(q, k, v, do, causal, policy=policy, disable=policy.PATH_FWD_HP)
     gen = _fwd_bwd(q, k, v, do, causal, policy=policy,
                    disable=policy.PATH_FWD_HP | policy.PATH_DQ_HP | policy.PATH_DKDV_HP)
-    for name, a, c in zip(("out", "dq", "dk", "dv"), hp, gen):
-        assert torch.isfinite(a).all(), name
-        assert torch.equal(a, c), f"{name}: max |diff| {(a.float() - c.float()).abs().max().item():.3e}"
+    assert_hp_vs_general(hp, gen)
 
 
 @pytest.mark.gpu
