@@ -60,10 +60,13 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PEAK_TFLOPS = 2500.0  # MI355X dense bf16/fp16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
-# Philox4x32-10 draws per second over the whole chip (bench_micro/philox_rate.hip, the library's
-# philox_uniform at full occupancy; profiles/r04g_philox_rate.txt): the VALU bound of the dropout
-# forward, which draws one uniform per visible (row, key) as the reference's tl.rand does
-PHILOX_DRAWS_PER_S = 8.9158e11
+# Philox4x32-10 draws per second over the whole chip: dropout_mask_kernel (misc.hip: all VALU, 38
+# instructions per draw, full occupancy) alone on the non-causal cfg3 mask, 4.29e9 draws in 4.331 ms
+# (profiles/r06i_dropout_fwd_kernel_trace.jsonl; round 4's philox_uniform microbench:
+# 8.92e11, profiles/r04g_philox_rate.txt) -- the VALU bound of the dropout forward, which draws one
+# uniform per visible (row, key) as the reference's tl.rand does
+PHILOX_DRAWS_PER_S = 9.918e11
+PHILOX_SOURCE = "dropout_mask_kernel alone, non-causal cfg3 (profiles/r06i_dropout_fwd_kernel_trace.jsonl)"
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md: ~8 TB/s)
 N_SIMDS = 1024  # 256 CUs x 4 SIMDs
 METRIC = "attention TFLOP/s (fwd & fwd+bwd) at S=4096 D=128 bf16; % of MFMA peak"
@@ -506,11 +509,13 @@ def main():
                                                                        True)
     dominant = max(times, key=lambda n: times[n])
     # device symbols the workload dispatches to, by the library's own conditions (the bench's tensors
-    # are contiguous, so every row is 16-byte aligned): forward -- fwd_hp_ok (D = 128, no bias, no
-    # dropout), else fwd_pipe_kernel (D in {64, 128}, no dropout, no bias or a 16-bit one:
-    # bias16_rows), else fwd_kernel; dQ / dK-dV -- dq_hp_ok / dkdv_hp_ok (D = 128, no bias; with
-    # dropout only through the forward's saved keep words, which this bench passes)
-    hp_fwd = d == 128 and bias is None and p_drop == 0.0
+    # are contiguous, so every row is 16-byte aligned): forward -- fwd_hp_ok (D = 128, no bias; with
+    # dropout only with a keep-mask buffer, which this bench passes: dropout_mask_kernel, then
+    # fwd_hp_kernel reading its words), else fwd_pipe_kernel (D in {64, 128}, no dropout, no bias
+    # or a 16-bit one: bias16_rows), else fwd_kernel (after dropout_mask_kernel with dropout);
+    # dQ / dK-dV -- dq_hp_ok / dkdv_hp_ok (D = 128, no bias; with dropout only through the
+    # forward's saved keep words)
+    hp_fwd = d == 128 and bias is None
     pipe_fwd = d in (64, 128) and p_drop == 0.0 and (bias is None or bias.dtype in (torch.float16, torch.bfloat16))
     hp_bwd = d == 128 and bias is None
     symbol = {"fwd_kernel": "fwd_hp_kernel" if hp_fwd else ("fwd_pipe_kernel" if pipe_fwd else "fwd_kernel"),
@@ -616,11 +621,12 @@ def main():
         vis = s * (s + 1) // 2 if causal else s * s
         draws = b * h * vis
         rate = draws / t_fwd
-        line["roofline_valu"] = {"bound": "valu", "kernel": "fa2::fwd_kernel", "achieved": round(rate, 1),
+        line["roofline_valu"] = {"bound": "valu", "kernel": f"fa2::dropout_mask_kernel + fa2::{symbol['fwd_kernel']}",
+                                 "achieved": round(rate, 1),
                                  "peak": PHILOX_DRAWS_PER_S, "unit": "Philox draws/s",
                                  "frac": round(rate / PHILOX_DRAWS_PER_S, 4), "draws_per_launch": draws,
                                  "bound_ms": round(draws / PHILOX_DRAWS_PER_S * 1e3, 4),
-                                 "peak_source": "bench_micro/philox_rate.hip (profiles/r04g_philox_rate.txt)"}
+                                 "peak_source": PHILOX_SOURCE}
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

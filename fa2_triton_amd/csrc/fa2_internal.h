@@ -27,6 +27,11 @@ hipError_t launch_bwd_dt(const fa2_bwd_args& a, bool aligned, int stages, hipStr
 hipError_t launch_cu_seqlens(const uint8_t* mask, int64_t stride, int batch, int seqlen,
                              int32_t* out, hipStream_t st);
 
+// Dropout keep words of a forward (misc.hip, into a.dropout_mask) drawn ahead of a kernel that
+// reads them; keep <=> the Philox integer x' > dropout_keep_threshold(p).
+uint32_t dropout_keep_threshold(float p);
+hipError_t launch_dropout_mask(const fa2_fwd_args& a, hipStream_t st);
+
 // q-head split of dK/dV (ABI 4): the smallest divisor s of the GQA group size G = Hq / Hkv with
 // s * B * Hkv * ceil(Sk / 128) >= kDkvTargetGrid workgroups (two per CU), G if none is; 1 when
 // G == 1 or the grid is already that large.

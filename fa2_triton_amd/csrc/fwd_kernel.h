@@ -44,9 +44,12 @@ struct FwdCfg {
 
 constexpr int kFwdLead = 3;  // fragment reads in flight ahead of their MFMA
 
-template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
+// DROP: 0 no dropout, 1 Philox draws in the softmax (writing the keep words when asked), 2 the keep
+// words a dropout_mask_kernel launch wrote just before (misc.hip) are read instead
+template <bool BF16, int DT, bool CAUSAL, bool BIAS, int DROP, bool ALIGNED>
 __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAUSAL>::kWavesPerSimd)) fwd_kernel(const fa2_fwd_args p) {
   using E = Elem<BF16>;
+  constexpr bool DROPOUT = DROP != 0;
   constexpr int NW = FwdCfg<DT, CAUSAL>::NW;
   constexpr bool PINGPONG = NW == 8;
   constexpr int NT = NW * 64;
@@ -141,6 +144,26 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
   // Scores are kept raw (no bias) or already in base-2 units (bias): exp2 argument = x*sc - m.
   const float sc = BIAS ? 1.f : scale2;
 
+  // DROP == 2: keep words of this lane's row for the two 32-key halves of a tile, loaded a tile
+  // ahead (mwn) and retired by the loop's waits before use (mwc)
+  uint32_t mwc[2] = {0u, 0u}, mwn[2] = {0u, 0u};
+  auto load_mw = [&](int n0) {
+    if constexpr (DROP == 2) {
+      const int nrb = (p.seqlen_q + 31) >> 5, ncw = (p.seqlen_k + 31) >> 5;
+      const int64_t rowbase = ((int64_t)bh * nrb + (qi >> 5)) * ncw;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        mwn[t] = (qi < p.seqlen_q && n0 + 32 * t < p.seqlen_k) ? p.dropout_mask[(rowbase + ((n0 >> 5) + t)) * 32 + (qi & 31)] : 0u;
+    }
+  };
+  auto next_mw = [&](int n0) {
+    if constexpr (DROP == 2) {
+      mwc[0] = mwn[0];
+      mwc[1] = mwn[1];
+      load_mw(n0 + BN);
+    }
+  };
+
   // state handed from a wave's QK phase to its PV phase
   u32x4 pf[2][2];
   float alpha = 1.f;
@@ -206,7 +229,12 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
         pv[i] = __builtin_amdgcn_exp2f(fmaf(s[t][i], sc, -m_use));
         rs += pv[i];
       }
-      if (DROPOUT) {
+      if (DROP == 2) {
+        // the word of the row's 32 keys (loaded a tile ahead); this lane's bits sit at 4 hh + ..
+        const uint32_t wd = mwc[t] >> (4 * hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pv[i] = ((wd >> ((i & 3) + 8 * (i >> 2))) & 1u) ? pv[i] : 0.f;
+      } else if (DROPOUT) {
         const uint64_t rowoff = drop_base + (uint64_t)qi * Lk;
         uint32_t kb = 0;  // keep bits of this lane's 16 keys at their positions in the 32-key word
 #pragma unroll
@@ -259,6 +287,7 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
     }
   };
 
+  load_mw(0);
   __builtin_amdgcn_s_waitcnt(0);  // prologue: Q fragments (compiler-tracked) + first tiles
   __syncthreads();
 
@@ -276,6 +305,7 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
     constexpr bool SPREAD = ALIGNED && NT == BN * 4;
     for (int i = 0; i < ntiles; ++i) {
       const int n0 = i * BN;
+      next_mw(n0);
       const uint16_t* kgt = kg + (int64_t)(n0 + BN) * p.k_stride[1];
       const uint16_t* vgt = vg + (int64_t)(n0 + BN) * p.v_stride[1];
       int64_t kadj = 0, vadj = 0;
@@ -328,6 +358,7 @@ __global__ void __launch_bounds__((FwdCfg<DT, CAUSAL>::NW * 64), (FwdCfg<DT, CAU
           const bool dead = CAUSAL && (n0 > qw0 + 31 + diag);
           const bool need_mask = (n0 + BN > Lk) || (CAUSAL && (n0 + BN - 1 > qw0 + diag));
           live = !dead;
+          next_mw(n0);
           if (!dead) {
             if (need_mask) qk_softmax(std::true_type{}, kt(tile & 1), n0, nofill);
             else qk_softmax(std::false_type{}, kt(tile & 1), n0, nofill);
@@ -391,7 +422,16 @@ template <bool BF16, int DT, bool CAUSAL, bool BIAS, bool DROPOUT, bool ALIGNED>
 static hipError_t launch_fwd_t(const fa2_fwd_args& a, hipStream_t st) {
   constexpr int NW = FwdCfg<DT, CAUSAL>::NW, BM = NW * 32;
   dim3 grid(((a.seqlen_q + BM - 1) / BM) * a.batch * a.heads_q);
-  hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT, ALIGNED>), grid, dim3(NW * 64), 0, st, a);
+  if constexpr (DROPOUT) {
+    // with a keep-mask buffer the bits are drawn by dropout_mask_kernel (all VALU, full
+    // occupancy) and read here; without one the softmax draws them
+    if (a.dropout_mask) {
+      if (hipError_t e = launch_dropout_mask(a, st); e != hipSuccess) return e;
+      hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, 2, ALIGNED>), grid, dim3(NW * 64), 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((fwd_kernel<BF16, DT, CAUSAL, BIAS, DROPOUT ? 1 : 0, ALIGNED>), grid, dim3(NW * 64), 0, st, a);
   return hipGetLastError();
 }
 

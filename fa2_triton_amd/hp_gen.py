@@ -285,6 +285,22 @@ REL = ["v208", "v209"]
 VNINF = "v210"
 TMP = ["v211", "v212", "v213", "v214", "v215"]
 N_VGPR = 216
+# dropout statement (exact scale only, where INIT(rb, 1..15) are unused): keep words W[set][rb][t]
+# of the lane's row (set = tile parity; t = 32-key half) in v[177:184], and per row block the byte
+# masks MC[rb][c] (byte n = 0xFF iff element (i & 3 = c, i >> 2 = n) is kept) in v[161:168];
+# s[92:95] the keep-mask descriptor, s96 the byte offset of the next tile's words
+FW_MD = "s[92:95]"
+FW_MT = "s96"
+FW_SEL = "s97"              # v_perm_b32 selector of the byte masks (mask_prep_items)
+FW_TMP = ["v169", "v170"]   # per row block: the S0 source of that v_perm_b32
+
+
+def FW_W(s, rb, t):
+    return f"v{177 + 4 * s + 2 * rb + t}"
+
+
+def FW_MC(rb, c):
+    return f"v{161 + 4 * rb + c}"
 
 
 def O(rb, dt, i=None):
@@ -420,8 +436,13 @@ class FwdGen:
     with -m_ref, so the chain yields z directly (no per-score VALU; costs one extra rounding of
     the scores, ~2^-9 relative in bf16)."""
 
-    def __init__(self, bf16, causal, exact=True, stamp=False, dt=128):
+    def __init__(self, bf16, causal, exact=True, stamp=False, dt=128, dropout=False):
         self.bf16, self.causal, self.exact, self.stamp = bf16, causal, exact, stamp
+        # dropout: P is multiplied by the keep bits a dropout_mask_kernel launch wrote just before
+        # (misc.hip) -- the packed P halves of dropped elements zeroed after the row sums (which
+        # are of the whole P, compute_row_blocks.py:76-79); 1 / (1 - p) in the epilogue
+        self.dropout = dropout
+        assert not (dropout and (stamp or dt != 128 or not exact))
         # head dim: 128 (8 k-steps, 4 d-tiles) or 64 (4, 2); a 64-row K / V tile is dt / 8 KiB,
         # staged in dt / 32 LDS-DMA pieces of 4 KiB
         self.dt, self.ks, self.ndt, self.np = dt, dt // 16, dt // 32, dt // 32
@@ -501,6 +522,53 @@ class FwdGen:
         r = f"v[{S(st, rb, t, i)[1:]}:{S(st, rb, t, i + 1)[1:]}]"
         l = f"v[{LSUM[rb][0][1:]}:{LSUM[rb][1][1:]}]"
         self.e.valu(f"v_pk_add_f32 {l}, {l}, {r}", l, [l, r])
+
+    # -- dropout keep words ----------------------------------------------------------------------
+    def word_load(self, s, rb, t):
+        """Keep word of the lane's row in block rb, 32-key half t, of the tile at byte offset s96
+        (tiled layout of fa2_amd.h: tile i at + 256 i, half t at + 128 t) -> W[s][rb][t]."""
+        self.e.raw(f"buffer_load_dword {FW_W(s, rb, t)}, %[mvo{rb}], {FW_MD}, {FW_MT} offen offset:{128 * t}")
+
+    def word_load_items(self, s):
+        """The next tile's four words -> set s (issue cost 8 each), then s96 moves one tile on."""
+        out = []
+        for n, (rb, t) in enumerate((rb, t) for rb in range(2) for t in range(2)):
+            def f(rb=rb, t=t, n=n):
+                self.word_load(s, rb, t)
+                if n == 3:
+                    self.e.salu(f"s_add_u32 {FW_MT}, {FW_MT}, 256")
+            out.append(f)
+        return out
+
+    def mask_prep_items(self, cur, rb, t):
+        """W >>= 4 hh (this lane's 16 keys at bits (i & 3) + 8 (i >> 2)); MC[rb][c] = the byte mask
+        whose byte n is 0xFF iff bit c + 8 n of W is set: v_perm_b32's sign selectors replicate
+        bits 15 / 31 of either source into a byte, so with S1 = W << (15 - c) (bits c, c + 16 at
+        15, 31) and S0 = W << (7 - c) (bits c + 8, c + 24 at 15, 31) the selector 0x0B090A08
+        (s97) builds it in one instruction (bench_micro/sdwa_sext_test.hip pins it)."""
+        e = self.e
+        w_ = FW_W(cur, rb, t)
+        tmp = FW_TMP[rb]
+        out = [lambda: e.valu(f"v_lshrrev_b32 {w_}, %[hh4], {w_}", w_, [w_])]
+        for c in range(4):
+            mc = FW_MC(rb, c)
+            out.append(lambda c=c, mc=mc: e.valu(f"v_lshlrev_b32 {mc}, {15 - c}, {w_}", mc, [w_]))
+            out.append(lambda c=c: e.valu(f"v_lshlrev_b32 {tmp}, {7 - c}, {w_}", tmp, [w_]))
+            out.append(lambda mc=mc: e.valu(f"v_perm_b32 {mc}, {tmp}, {mc}, {FW_SEL}", mc, [tmp, mc]))
+        return out
+
+    def mask_and(self, rb, kk, j, h):
+        """Zero half h of the P pack PF[rb][kk][j] (element i = 8 (kk & 1) + 2 j + h) unless its keep
+        bit is set: AND with the sign-extended byte i >> 2 (0x00 / 0xFF) of MC[rb][i & 3] (SDWA
+        writes the low 16 bits of the result to the selected word: P's word is selected on the
+        source too; a byte's sign extension keeps its low 7 bits, hence whole-byte masks)."""
+        i = 8 * (kk & 1) + 2 * j + h
+        pp, mc = PF(rb, kk, j), FW_MC(rb, i & 3)
+        self.e.valu(f"v_and_b32_sdwa {pp}, sext({mc}), {pp} dst_sel:WORD_{h} dst_unused:UNUSED_PRESERVE "
+                    f"src0_sel:BYTE_{i >> 2} src1_sel:WORD_{h}", pp, [mc, pp])
+
+    def mask_and_items(self, rb, kk):
+        return [lambda j=j, h=h: self.mask_and(rb, kk, j, h) for j in range(4) for h in range(2)]
 
     def mask_elem(self, st, rb, t, i):
         """z = key offset o < rel[rb] ? z : -inf  (o = 32 t + (i & 3) + 8 (i >> 2))."""
@@ -843,6 +911,17 @@ class FwdGen:
             rb_, kk_, j_ = c
             idx = [16 * kk_ + 8 * rb_ + 2 * j_, 16 * kk_ + 8 * rb_ + 2 * j_ + 1]
             gx.add("cvt", 4, min(nx - 1, after(idx, x_dl)), nx - 1, lambda c=c: self.cvt(cur, *c))
+        if self.dropout:
+            # (class C only at D = 128, where A / B take period_xy_bal: phase X has no MFMA, so its
+            # items run in list order after the first gap's -- released past it -- every pack first)
+            assert not qk
+            for rb in range(2):
+                for t in range(2):
+                    for f in self.mask_prep_items(cur, rb, t):
+                        gx.add("dm", 4, 0, nx - 1, f)
+                    for kk in (2 * t, 2 * t + 1):
+                        for f in self.mask_and_items(rb, kk):
+                            gx.add("dm", 4, 0, nx - 1, f)
         for m in range(LEADV):
             for h in range(2):
                 gx.add("vr", 4, max(0, nx - 12), nx - 1, lambda m=m, h=h: self.v_read(vbuf, m, h))
@@ -993,12 +1072,23 @@ class FwdGen:
             gxa("exp", 8, x_dl[n] - 1, x_dl[n], lambda el=E[n]: self.exp(cur, el))
         for n, f in enumerate(dma):
             gxa("dma", f[0], -1, min(nx - 1, (4 * n + 3) * nx // 32), f[1])
+        # dropout: the kk = 0 packs early enough for their keep masking in phase X (X_CVT0); the
+        # next tile's keep words requested at the period start
+        X_CVT0 = 20
         for kk in (0, 1):
             for rb in range(2):
                 for j in range(4):
                     idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
-                    gxa(f"cvt{kk}", 4, max(x_dl[i] for i in idx) + 1, nx - 1,
+                    gxa(f"cvt{kk}", 4, max(x_dl[i] for i in idx) + 1, X_CVT0 if self.dropout and kk == 0 else nx - 1,
                         lambda c=(rb, kk, j): self.cvt(cur, *c))
+        if self.dropout:
+            for f in self.word_load_items(nxt):
+                gxa("wl", 8, -1, 6, f)
+            for rb in range(2):
+                for f in self.mask_prep_items(cur, rb, 0):
+                    gxa(f"dm{rb}", 4, -1, X_CVT0 - 2, f)
+                for f in self.mask_and_items(rb, 0):
+                    gxa(f"dm{rb}", 4, X_CVT0 + 1, nx - 1, f)
         if "fw_pk" in ABL:  # (A/B: row sums of element pairs by v_pk_add_f32, same partial sums)
             for n in range(0, 16, 2):
                 gxa("add", 8, max(x_dl[n], x_dl[n + 1]) + 1, nx - 1, lambda el=E[n]: self.add_pk(cur, el))
@@ -1032,16 +1122,29 @@ class FwdGen:
             if m + LEADV < nv:
                 for h in range(2):
                     gy.add("v", 4, 2 * m, 2 * m + 1, lambda m=m, h=h: self.v_read(vbuf, m + LEADV, h))
-        y_dl = {n: ((n - n_x) * 20) // (64 - n_x) for n in range(n_x, 64)}
+        # (dropout: exponentials and packs earlier, so that the keep masking of a pack fits between
+        # it and the first PV MFMA reading it, MFMA 8 kk)
+        y_span = 16 if self.dropout else 20
+        y_dl = {n: ((n - n_x) * y_span) // (64 - n_x) for n in range(n_x, 64)}
         for n in range(n_x, 64):
             gy.add("exp", 8, y_dl[n] - 1, y_dl[n], lambda el=E[n]: self.exp(cur, el))
         # packs of P(kk) before the first PV MFMA reading them (MFMA 8 kk; margin for VALU -> MFMA)
+        y_cvt = (9, 17) if self.dropout else (13, 21)
         for kk in (2, 3):
             for rb in range(2):
                 for j in range(4):
                     idx = [16 * kk + 8 * rb + 2 * j, 16 * kk + 8 * rb + 2 * j + 1]
                     rel = max([y_dl[i] for i in idx if i in y_dl] + [-2]) + 1
-                    gy.add(f"cvt{kk}", 4, rel, (13, 21)[kk - 2], lambda c=(rb, kk, j): self.cvt(cur, *c))
+                    gy.add(f"cvt{kk}", 4, rel, y_cvt[kk - 2], lambda c=(rb, kk, j): self.cvt(cur, *c))
+        if self.dropout:
+            for rb in range(2):
+                for f in self.mask_and_items(rb, 1):
+                    gy.add(f"dm{rb}", 4, -1, 5, f)
+                for f in self.mask_prep_items(cur, rb, 1):
+                    gy.add(f"dm{rb}", 4, -1, 8, f)
+                for kk in (2, 3):
+                    for f in self.mask_and_items(rb, kk):
+                        gy.add(f"dm{rb}", 4, y_cvt[kk - 2] + 1, 8 * kk - 2, f)
         if "fw_pk" in ABL:
             for n in range(16, 64, 2):
                 rel = max(y_dl.get(n, -2), y_dl.get(n + 1, -2)) + 1
@@ -1141,6 +1244,19 @@ class FwdGen:
         e.salu(f"s_mov_b32 {SI}, 0")
         e.salu(f"s_mov_b32 {SN1}, 0")
         e.salu(f"s_mov_b32 {SPAR}, %[boff]")
+        if self.dropout:
+            # the keep-mask descriptor; tile 0's words into both sets (its period's parity is boff)
+            e.salu("s_mov_b32 s92, %[mlo]")
+            e.salu("s_mov_b32 s93, %[mhi]")
+            e.salu("s_mov_b32 s94, %[mbytes]")
+            e.salu("s_mov_b32 s95, 0x20000")
+            e.salu(f"s_mov_b32 {FW_MT}, 0")
+            e.salu(f"s_mov_b32 {FW_SEL}, 0x0b090a08")
+            for s_ in range(2):
+                for rb in range(2):
+                    for t in range(2):
+                        self.word_load(s_, rb, t)
+            e.salu(f"s_mov_b32 {FW_MT}, 256")
         # this unit's K(0), V(0), K(1) and Q (requested during the previous unit's final period,
         # or before the statement) have landed
         e.raw("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -2590,14 +2706,14 @@ FA2_DEV void dq_hp_load_next(u32x4 (&q)[16], u32x4 (&o)[16], const DqHpArgs& a) 
 """
 
 
-def gen_fwd_function(bf16, causal, exact=True, dt=128):
+def gen_fwd_function(bf16, causal, exact=True, dt=128, dropout=False):
     out = []
     nq = 2 * (dt // 16)  # Q fragments (two row blocks x k-steps)
-    for stamp in (False, True):
-        g = FwdGen(bf16, causal, exact, stamp, dt)
+    for stamp in ((False,) if dropout else (False, True)):
+        g = FwdGen(bf16, causal, exact, stamp, dt, dropout)
         lines = g.build()
         name = f"fwd_hp_main_{'bf16' if bf16 else 'f16'}_{'causal' if causal else 'full'}{'' if exact else '_ps'}" + \
-            ("" if dt == 128 else f"_d{dt}")
+            ("" if dt == 128 else f"_d{dt}") + ("_drop" if dropout else "")
         # O^T a[0 : dt], K / V^T rings a[192:223]; every AGPR but the Q operands' (a[128:191] at
         # D = 128, a[64:95] at D = 64) clobbered, so the compiler has no room to move them
         acc = list(range(0, dt)) + list(range(dt + 2 * dt // 4 if dt == 64 else 192, 256))
@@ -2606,15 +2722,17 @@ def gen_fwd_function(bf16, causal, exact=True, dt=128):
         qops = ", ".join(f'[q{i}] "+a"(q[{i}])' for i in range(nq))
         stops = ", " + ", ".join(f'[st{i}] "=&s"(st[{i}])' for i in range(4)) if stamp else ""
         starg = ", uint32_t (&st)[4]" if stamp else ""
+        dops = ('\n        [mvo0] "v"(a.mvo[0]), [mvo1] "v"(a.mvo[1]), [hh4] "v"(a.hh4), [mlo] "s"(a.mlo), '
+                '[mhi] "s"(a.mhi), [mbytes] "s"(a.mbytes),' if dropout else "")
         out.append(f"""{'#if FA2_HP_STAMPS' if stamp else '#if !FA2_HP_STAMPS'}
-// hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}{', stamped' if stamp else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
+// hand-placed unit ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}, {'exact scale' if exact else 'pre-scaled Q'}{', dropout' if dropout else ''}{', stamped' if stamp else ''}): {len(lines)} lines, {g.e.n_mfma} MFMAs
 // q: this unit's Q fragments in, the NEXT unit's Q fragments out -- still in flight (the next
 // statement waits for them first; nothing may read q in between)
 FA2_DEV void {name}(u32x4 (&q)[{nq}], const FwdHpArgs& a, float (&m_out)[2], float (&l_out)[2]{starg}) {{
   asm volatile(
 {_asm_body(lines)}
       : [mo0] "=&v"(m_out[0]), [mo1] "=&v"(m_out[1]), [lo0] "=&v"(l_out[0]), [lo1] "=&v"(l_out[1]), {qops}{stops}
-      : [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),
+      : [kb0] "v"(a.kb0), [kb1] "v"(a.kb1), [va] "v"(a.va), [vb] "v"(a.vb),{dops}
         {", ".join(f'[off{i}] "v"(a.off[{i}])' for i in range(dt // 32))},
         [rel0] "v"(a.rel[0]), [rel1] "v"(a.rel[1]), [nqo0] "v"(a.nqo[0]), [nqo1] "v"(a.nqo[1]),
         [na] "s"(a.na), [last] "s"(a.last), [ntiles] "s"(a.ntiles), [mask0] "s"(a.mask0),
@@ -2658,6 +2776,7 @@ def write_headers():
         for causal in (True, False):
             for exact in (True, False):
                 out.append(gen_fwd_function(bf16, causal, exact))
+            out.append(gen_fwd_function(bf16, causal, True, dropout=True))
             # (FwdGen(dt=64) builds a D = 64 unit too; measured no faster than fwd_pipe_kernel at
             # D = 64, where the softmax VALU bounds both -- DESIGN.md section 6 -- so not emitted)
     out.append(gen_read_o())

@@ -74,7 +74,10 @@ typedef struct fa2_fwd_args {
    * one 128-byte tile of slack the backward may read past the last one), so that the backward reads
    * them instead of regenerating Philox (fa2_bwd_args.dropout_mask).  Layout: 32 x 32 bit tiles,
    * word[((b * Hq + h) * ceil(Sq / 32) + i / 32) * ceil(Sk / 32) + j / 32][i % 32], bit j % 32 =
-   * keep(b, h, i, j).  Only the tiles the (causal) mask leaves visible are written. */
+   * keep(b, h, i, j).  Only the tiles the (causal) mask leaves visible are written.  The buffer is
+   * also the forward's input: with it the forward first draws every visible word (an all-VALU
+   * Philox launch) and then reads them (the D = 128 hand-placed forward runs with dropout only
+   * then); O equals the no-buffer forward's within rounding, not bitwise. */
   uint32_t* dropout_mask;
 } fa2_fwd_args;
 

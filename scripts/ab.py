@@ -1,7 +1,8 @@
 """A/B timing of several libfa2_amd.so builds in ONE process (interleaved rounds), cfg3 causal.
 
 usage: python scripts/ab.py lib_a.so lib_b.so[:ENV=VAL,...] [...]   (env CAUSAL=0 for non-causal, WHAT=fwd,bwd,
-       SHAPE=B,H,S,D; a ":ENV=VAL" suffix sets those variables while that arm runs)
+       SHAPE=B,H,S,D, DROPOUT=p (the forward saves its keep words, the backward reads them); a
+       ":ENV=VAL" suffix sets those variables while that arm runs)
 WHAT: fwd | dkdv, dq (backward stages) | bwd (whole backward)
 """
 import ctypes
@@ -15,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import fa2_triton_amd._lib as L  # noqa: E402
 from fa2_triton_amd.backward import _flash_attn_backward  # noqa: E402
 from fa2_triton_amd.forward import _flash_attn_forward  # noqa: E402
+from fa2_triton_amd.utils import dropout_mask_words  # noqa: E402
 
 libs = []
 envs = {}
@@ -34,6 +36,9 @@ q = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 k = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 v = torch.empty(b, s, h, d, device="cuda", dtype=torch.bfloat16).normal_(0, 0.5)
 do = torch.randn_like(q)
+pd = float(os.environ.get("DROPOUT", "0"))
+seed = 1234 if pd > 0 else None
+kmask = torch.empty(dropout_mask_words(b, h, s, s), dtype=torch.int32, device="cuda") if pd > 0 else None
 F = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
 flops = {"fwd": F, "dkdv": 2 * F, "dq": 1.5 * F, "bwd": 2.5 * F}
 results = {(n, w): [] for n, _ in libs for w in what}
@@ -44,14 +49,15 @@ for rnd in range(5):
             for k_ in kv:
                 os.environ.pop(k_, None)
         os.environ.update(envs[name])
-        o, lse, _, _ = _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None)
+        fw = dict(dropout_mask=kmask)
+        o, lse, scale, _ = _flash_attn_forward(q, k, v, None, None, pd, causal, None, seed, **fw)
         delta = torch.empty_like(lse)
-        _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=1, _delta=delta)
+        _flash_attn_backward(do, q, k, v, None, None, o, lse, pd, causal, scale, seed, _stages=1, _delta=delta, **fw)
         calls = {
-            "fwd": lambda: _flash_attn_forward(q, k, v, None, None, 0.0, causal, None, None),
-            "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=2, _delta=delta),
-            "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None, _stages=4, _delta=delta),
-            "bwd": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, 0.0, causal, None, None),
+            "fwd": lambda: _flash_attn_forward(q, k, v, None, None, pd, causal, None, seed, **fw),
+            "dkdv": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, pd, causal, scale, seed, _stages=2, _delta=delta, **fw),
+            "dq": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, pd, causal, scale, seed, _stages=4, _delta=delta, **fw),
+            "bwd": lambda: _flash_attn_backward(do, q, k, v, None, None, o, lse, pd, causal, scale, seed, **fw),
         }
         for w in what:
             calls[w]()

@@ -119,7 +119,7 @@ def test_every_kernel_fits_the_cu(kernels):
 
 # the hand-placed one-wave-per-SIMD kernels (hp_gen.py): whole register file, zero scratch
 HP = {
-    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb1ELi128EEEv12fa2_fwd_args",
+    "fwd_hp": r"_ZN3fa213fwd_hp_kernelILb[01]ELb[01]ELb1ELi128ELb[01]EEEv12fa2_fwd_args",
     "dkdv_hp": r"_ZN3fa214dkdv_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_bwd_argsi",
     "dq_hp": r"_ZN3fa212dq_hp_kernelILb[01]ELb[01]ELb[01]EEEv12fa2_bwd_args",
 }
@@ -129,9 +129,9 @@ HP = {
 def test_hand_placed_kernels_have_no_scratch(kernels, kind):
     pat = re.compile(HP[kind] + "$")
     found = {k: v for k, v in kernels.items() if pat.match(k)}
-    # dtypes x causal (x dropout for dQ and dK/dV; the pre-scaled-Q forward exists only in
-    # development builds, FA2_HP_DEV)
-    assert len(found) == (4 if kind == "fwd_hp" else 8), (kind, sorted(found))
+    # dtypes x causal x dropout (the pre-scaled-Q forward exists only in development builds,
+    # FA2_HP_DEV)
+    assert len(found) == 8, (kind, sorted(found))
     for k, (scratch, vgprs, lds) in found.items():
         assert scratch == 0, (k, scratch)
         assert vgprs <= 512 and lds <= 160 * 1024, (k, vgprs, lds)  # one workgroup of 4 waves per CU

@@ -206,3 +206,46 @@ def test_dropout_hand_placed_dkdv(b, hq, hkv, sq, sk, causal, p, dtype, cap, pol
     policy.set_path_policy(0, 0)
     assert_dropout_grads_match(hp[:3], gen[:3])
     assert_dropout_dv_vs_oracle(hp[2], gen[2], q, k, v, do, words, p, causal)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [0, 2])
+@pytest.mark.parametrize("b,hq,hkv,sq,sk,causal,p,dtype", DROP_CASES, ids=lambda x: str(x).replace("torch.", ""))
+def test_dropout_hand_placed_forward(b, hq, hkv, sq, sk, causal, p, dtype, cap, policy):
+    """The dropout forward at D = 128 (round 6): dropout_mask_kernel draws the keep words (integer
+    threshold on the Philox word), fwd_hp_kernel's dropout statement reads them and zeroes the
+    dropped P halves after the row sums.  The words equal the Philox oracle's mask on every visible
+    element; O and LSE2 against the fp32 oracle over those bits (O = (P * M / (1 - p)) V / l,
+    compute_row_blocks.py:76-79), within the bound of the general kernel reading the same words;
+    several units per workgroup (cap 2) bitwise equal to one unit each."""
+    from fa2_triton_amd.forward import _flash_attn_forward
+    from fa2_triton_amd.utils import dropout_mask_words
+    from oracle.philox import dropout_keep_mask_torch
+    from oracle.reference import attention_reference, lse2_reference
+    from tests.core import unpack_keep_mask
+
+    q, k, v, _ = generate_test_data(b, hq, hkv, sq, sk, 128, dtype)
+    res = {}
+    for tag, dis, cp in (("hp", 0, cap), ("hp1", 0, 0), ("gen", policy.PATH_FWD_HP, 0)):
+        words = torch.full((dropout_mask_words(b, hq, sq, sk),), -1, dtype=torch.int32, device=q.device)
+        policy.set_path_policy(dis, cp)
+        o, lse, _, seed = _flash_attn_forward(q, k, v, None, None, p, causal, None, 777, dropout_mask=words)
+        policy.set_path_policy(0, 0)
+        res[tag] = (o, lse[:, :, :sq].float(), words)
+    assert torch.equal(res["hp"][0], res["hp1"][0]) and torch.equal(res["hp"][1], res["hp1"][1])
+    keep = unpack_keep_mask(res["hp"][2], b, hq, sq, sk)
+    vis = torch.ones(sq, sk, dtype=torch.bool, device=q.device)
+    if causal:
+        vis = torch.arange(sk, device=q.device)[None, :] <= torch.arange(sq, device=q.device)[:, None] + (sk - sq)
+    want = dropout_keep_mask_torch(seed, p, b, hq, sq, sk, device=q.device)
+    assert torch.equal(keep[:, :, vis], want[:, :, vis])
+    ref = attention_reference(q, k, v, dropout_p=p, dropout_mask=keep, causal=causal).float()
+    e_gen = (res["gen"][0].float() - ref).abs().max().item()
+    e_hp = (res["hp"][0].float() - ref).abs().max().item()
+    assert e_hp <= 2 * e_gen + 5e-5, f"hp {e_hp:.3e} vs general {e_gen:.3e}"
+    lref = lse2_reference(q, k, causal=causal)
+    fin = torch.isfinite(lref)
+    lse = res["hp"][1]
+    assert torch.equal(torch.isfinite(lse), fin)
+    if fin.any():
+        assert (lse[fin] - lref[fin]).abs().max().item() <= 1e-3 * (1 + lref[fin].abs().max().item())
