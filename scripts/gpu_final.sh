@@ -7,10 +7,15 @@ TAG=${1:-r04h}
 OUT=gpurun_out/final_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+# PART=tests | bench (default both: one call may not hold both within gpurun's limit)
+PART=${PART:-all}
+if [ "$PART" != bench ]; then
 FA2_TOL_REPORT=$OUT/tolerance_escapes.txt timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -20 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
+[ "$PART" = tests ] && exit 0
+fi
 bash scripts/profile_round.sh $TAG || exit $?
 for leg in "" "--no-causal" "--dropout 0.1" "--bias" "--config cfg2" "--config refbench" "--config cfg5" "--bias-grad --steps 3 --warmup 1"; do
   f=$OUT/bench_$(echo "x$leg" | tr -d ' -.').json

@@ -10,6 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 RK="python3 scripts/run_kernels.py --reps 3"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/bench -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_stdout.txt 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/bench_dropout -o run --output-format csv -- python3 bench.py --dropout 0.1 --no-cpu-baseline > $OUT/bench_dropout_stdout.txt 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $RK > $OUT/fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $RK > $OUT/write.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $OUT/sq1 -o run --output-format csv -- $RK > $OUT/sq1.log 2>&1 || exit $?

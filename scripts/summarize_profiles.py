@@ -13,6 +13,8 @@ dst = "profiles"
 os.makedirs(dst, exist_ok=True)
 stats = glob.glob(f"{src}/bench/**/*kernel_stats.csv", recursive=True)[0]
 shutil.copy(stats, f"{dst}/{tag}_bench_kernel_stats.csv")
+for f in glob.glob(f"{src}/bench_dropout/**/*kernel_stats.csv", recursive=True)[:1]:
+    shutil.copy(f, f"{dst}/{tag}_bench_dropout_kernel_stats.csv")
 
 
 def counters(sub):
