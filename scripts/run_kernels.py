@@ -19,7 +19,11 @@ ap.add_argument("--s", type=int, default=4096)
 ap.add_argument("--d", type=int, default=128)
 ap.add_argument("--causal", type=int, default=1)
 ap.add_argument("--dtype", default="bf16")
+ap.add_argument("--disable", type=int, default=0, help="fa2_policy.disable bits (PATH_FWD_HP = 1, ...)")
 a = ap.parse_args()
+if a.disable:
+    from fa2_triton_amd import _lib as L
+    L.set_path_policy(a.disable, 0)
 dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
 hkv = a.hkv or a.h
 torch.manual_seed(0)
