@@ -590,7 +590,10 @@ FA2_DEV u32x4 load_row_frag(const uint16_t* row, int d0, int D, bool valid) {
 // not stored (D % 8 == 0).  The caller guarantees no other wave still reads `stage`.
 template <bool BF16, int DT>
 FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool valid, uint16_t* g0, int64_t rstride,
-                            int nrows, int D, int lane) {
+                            int nrows, int D, int lane, uint64_t* tacc = nullptr) {
+#if FA2_HP_STAMPS
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
   using E = Elem<BF16>;
   constexpr int NDT = DT / 32;
   constexpr int CPR = DT / 8;   // 16-byte chunks per row
@@ -616,6 +619,13 @@ FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool vali
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if FA2_HP_STAMPS
+  if (tacc) {  // (development stamp builds: pack + LDS write, read back, global stores)
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    tacc[0] += t - t0;
+    t0 = t;
+  }
+#endif
   const int c = lane % CPR;
   // every row read issued before the first store (one LDS wait, not one per store)
   u32x4 v[32 / RPI];
@@ -625,11 +635,21 @@ FA2_DEV void store_rows_lds(char* stage, const f32x16* acc, float mul, bool vali
     v[j] = *(const u32x4*)(stage + R * (DT * 2) + 16 * (c ^ (R % CPR)));
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if FA2_HP_STAMPS
+  if (tacc) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    tacc[1] += t - t0;
+    t0 = t;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < 32 / RPI; ++j) {
     const int R = j * RPI + lane / CPR;
     if (R < nrows && 8 * c < D) *(u32x4*)(g0 + (int64_t)R * rstride + 8 * c) = v[j];
   }
+#if FA2_HP_STAMPS
+  if (tacc) tacc[2] += __builtin_amdgcn_s_memtime() - t0;
+#endif
 }
 
 // a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the backend emits two v_xor_b32 here.

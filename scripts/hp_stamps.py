@@ -59,6 +59,10 @@ def run_one(lib_path, cases):
             rec[name + "_cyc_per_period"] = round(st[i] / waves / periods, 1)
         rec["rest_cyc_per_unit"] = round((st[3] - st[0] - st[1] - st[2]) / waves, 1)
         rec["epilogue_cyc_per_unit"] = round(st[4] / waves, 1)
+        # the epilogue's parts: accumulator read-out, then each 32-row block (1 / l, LSE, staging, stores)
+        for name, i in (("readout", 6), ("block0", 7), ("block1", 8), ("pack_ldswrite", 9), ("readback", 10),
+                        ("stores", 11)):
+            rec[name + "_cyc_per_unit"] = round(st[i] / waves, 1)
         # cycles per SIMD per launch (one wave per SIMD) over the launch time: the in-kernel clock
         rec["clock_ghz"] = round((st[3] + st[4]) / 1024 / reps / (rec["ms"] * 1e6), 3)
         print(json.dumps(rec), flush=True)
