@@ -749,8 +749,12 @@ struct DqCfg {
 // (fwd_pipe_kernel.h): each wave's [32 rows x 64 keys] bias tile of tile i goes out first at the
 // top of tile i and is waited for (counted vmcnt, the next K/V tile left in flight) right before
 // the softmax gradient of its first key half.
+#ifndef FA2_DQ_BIAS_WPS
+#define FA2_DQ_BIAS_WPS 2
+#endif
 template <bool BF16, int DT, bool CAUSAL, int BIASK, bool DROPOUT, bool ALIGNED, bool DQF32>
-__global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) dq_kernel(const fa2_bwd_args p) {
+__global__ void __launch_bounds__(DqCfg<DT>::NW * 64, BIASK != 0 && DT == 128 ? FA2_DQ_BIAS_WPS : DqCfg<DT>::kWavesPerSimd)
+    dq_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
   constexpr bool BIAS = BIASK != 0, BIASL = BIASK >= 16;
   constexpr int NW = DqCfg<DT>::NW;
@@ -1173,7 +1177,10 @@ __global__ void __launch_bounds__(DqCfg<DT>::NW * 64, DqCfg<DT>::kWavesPerSimd) 
 // 64-key tiles per dbias workgroup.  One: the block's sums and bias (32 + 32 fp32 per lane) leave
 // the arch VGPRs room to read the K/V fragments ahead of the MFMAs; with two (64 + 64) the
 // compiler read each fragment just before its MFMA and waited out the LDS latency every time.
-constexpr int kDbiasChunk = 1;
+#ifndef FA2_DBIAS_CHUNK
+#define FA2_DBIAS_CHUNK 1
+#endif
+constexpr int kDbiasChunk = FA2_DBIAS_CHUNK;
 
 // XCD-aware block order: workgroup g runs on XCD g % 8 as that XCD's (g / 8)-th; the blocks go
 // out in 8 x 8 squares of (row block, key chunk), so the workgroups an XCD runs together share
@@ -1199,6 +1206,57 @@ FA2_DEV void dbias_block(int g, int nmb, int nkc, int& mb, int& kc) {
   mb = r * e + within / e;
   kc = c * e + within % e;
   if (c >= sqk || mb >= nmb || kc >= nkc) mb = -1;
+}
+
+// Causal: an XCD's visible blocks first, in the square order above, then its empty ones.  Under the
+// plain order the empty blocks (above the diagonal, gone in microseconds) sat among the visible
+// ones, so an XCD's workgroups started their blocks at scattered times and walked the pairs out of
+// step: the Q / dO and K / V rows one workgroup fetched for a pair had left the L2 before the
+// others sharing them reached that pair.  Visible first, the 32 workgroups an XCD runs at once
+// start together on neighbouring blocks and stay in step (equal work per block).  The order is a
+// speed choice only: every block still decides per pair what it sees (varlen included).
+// dbias_lim: the key chunks row block mb sees at the padded lengths (a prefix kc < lim)
+__host__ __device__ inline int dbias_lim(int mb, int nkc, int Lq, int Lk) {
+  if (mb * 128 >= Lq) return 0;
+  const int n_end = max(min(Lk, (mb + 1) * 128 + Lk - Lq), 0);
+  return min(nkc, (n_end + 64 * kDbiasChunk - 1) / (64 * kDbiasChunk));
+}
+__host__ __device__ inline void dbias_block_visible_first(int g, int nmb, int nkc, int Lq, int Lk, int& mb, int& kc) {
+  const int e = dbias_side(nmb, nkc);
+  const int x = g & 7, j = g >> 3;
+  const int sqr = (nmb + e - 1) / e, sqk = (nkc + e - 1) / e, per_row = (sqk + 7) / 8;
+  const int nsq = sqr * per_row;  // the XCD's squares q = r per_row + m, column c = ((x - r) & 7) + 8 m
+  // blocks of square q's row i: valid chunks [lo, hi), the visible ones a prefix of nv
+  auto row = [&](int q, int i, int& m_, int& lo, int& hi, int& nv) {
+    const int r = q / per_row, c = ((x - r) & 7) + 8 * (q - r * per_row);
+    m_ = r * e + i;
+    lo = c * e;
+    hi = (c < sqk && m_ < nmb) ? min(lo + e, nkc) : lo;
+    nv = min(max(dbias_lim(m_, nkc, Lq, Lk) - lo, 0), hi - lo);
+  };
+  int nvis = 0;
+  for (int q = 0; q < nsq; ++q)
+    for (int i = 0; i < e; ++i) {
+      int m_, lo, hi, nv;
+      row(q, i, m_, lo, hi, nv);
+      nvis += nv;
+    }
+  const bool vis = j < nvis;
+  int rem = vis ? j : j - nvis;
+  mb = -1;
+  kc = 0;
+  for (int q = 0; q < nsq; ++q)
+    for (int i = 0; i < e; ++i) {
+      int m_, lo, hi, nv;
+      row(q, i, m_, lo, hi, nv);
+      const int cnt = vis ? nv : hi - lo - nv;
+      if (rem < cnt) {
+        mb = m_;
+        kc = lo + (vis ? 0 : nv) + rem;
+        return;
+      }
+      rem -= cnt;
+    }
 }
 
 template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
@@ -1227,7 +1285,10 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
   const int nkt = (p.seqlen_k + BN - 1) / BN;        // key tiles of the output rows
   const int nkc = (nkt + C - 1) / C;
   int mb, kc;
-  dbias_block(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, mb, kc);
+  if (CAUSAL)
+    dbias_block_visible_first(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, p.seqlen_q, p.seqlen_k, mb, kc);
+  else
+    dbias_block(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, mb, kc);
   if (mb < 0) return;                                // grid padding
   const int t0 = kc * C, t1 = min(nkt, t0 + C);     // this workgroup's key tiles
   const int Hb = p.bias_stride[1] != 0 ? p.heads_q : 1;
@@ -1276,14 +1337,45 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
         }
   }
 
+  // The pair cursor: the pair's index with its (batch, q-head, kv-head) carried along, so a step
+  // moves it by increments (index -> (b, hq) -> kv-head by division costs ~25 instructions per
+  // division, seven per step, on a one-wave-per-SIMD kernel whose step is short).  Pair order:
+  // index = b nh + hq over the summed dims (as the dims of the bias's broadcast group).
+  const int group = p.heads_q / p.heads_kv;
+  struct Cur {
+    int i, b, hq, hkv, gi;  // gi = hq - hkv group
+  };
+  Cur first;
+  first.i = 0;
+  first.b = sum_b ? 0 : bb;
+  first.hq = sum_h ? 0 : hb;
+  first.hkv = first.hq / group;
+  first.gi = first.hq - first.hkv * group;
+  auto step_cur = [&](Cur c) {
+    ++c.i;
+    if (sum_h) {
+      if (++c.gi == group) {
+        c.gi = 0;
+        ++c.hkv;
+      }
+      if (++c.hq == nh) {
+        c.hq = c.hkv = c.gi = 0;
+        ++c.b;
+      }
+    } else {
+      ++c.b;  // (a single pair when neither dim is summed: past the end)
+    }
+    return c;
+  };
   // the pair's visible key tiles are [t0, tend); a pair with none adds nothing
   struct Pair {
-    int b, hq, Lq, Lk, tend;
+    int b, hq, hkv, Lq, Lk, tend;
   };
-  auto pair_at = [&](int pair) {
+  auto pair_of = [&](const Cur& c) {
     Pair r;
-    r.b = sum_b ? pair / nh : bb;
-    r.hq = sum_h ? (sum_b ? pair - (pair / nh) * nh : pair) : hb;
+    r.b = c.b;
+    r.hq = c.hq;
+    r.hkv = c.hkv;
     r.Lq = p.seqlen_q;
     r.Lk = p.seqlen_k;
     if (p.cu_seqlens) r.Lq = r.Lk = p.cu_seqlens[r.b + 1] - p.cu_seqlens[r.b];
@@ -1292,14 +1384,13 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
     r.tend = min(t1, (n_end + BN - 1) / BN);
     return r;
   };
-  auto next_visible = [&](int pair) {
-    while (pair < np && pair_at(pair).tend <= t0) ++pair;
-    return pair;
+  auto next_visible = [&](Cur c) {
+    while (c.i < np && pair_of(c).tend <= t0) c = step_cur(c);
+    return c;
   };
   auto stage_kv = [&](int buf, const Pair& r, int n) {
-    const int hkv = r.hq / (p.heads_q / p.heads_kv);
-    const uint16_t* kg = (const uint16_t*)p.k + r.b * p.k_stride[0] + hkv * p.k_stride[2];
-    const uint16_t* vg = (const uint16_t*)p.v + r.b * p.v_stride[0] + hkv * p.v_stride[2];
+    const uint16_t* kg = (const uint16_t*)p.k + r.b * p.k_stride[0] + r.hkv * p.k_stride[2];
+    const uint16_t* vg = (const uint16_t*)p.v + r.b * p.v_stride[0] + r.hkv * p.v_stride[2];
     if constexpr (ALIGNED) {
       kst.issue(kt(buf), kg, p.k_stride[1], n, r.Lk, mrows);
       kst.issue(vt(buf), vg, p.v_stride[1], n, r.Lk, mrows);
@@ -1321,33 +1412,53 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
       }
     }
   };
+  // the lane's row of the pair's LSE2 and -delta (row 0 exists: Lq > 0)
+  auto rowstats = [&](const Pair& r, float& l, float& d) {
+    const int64_t srow = (int64_t)(r.b * p.heads_q + r.hq) * p.lse_row_stride + (qi < r.Lq ? qi : 0);
+    l = p.lse[srow];
+    d = p.delta[srow];
+  };
 
-  int pair = next_visible(0);
+  Cur cur = next_visible(first);
   int buf = 0;
   // staging cursor (pair, tile) of the K/V ring, RING - 1 steps ahead of the compute; past the
   // last pair it re-stages a tile of the current pair (unused) so every step issues the same loads
-  int spair = pair, sc = 0;
+  Cur scur = cur;
+  int sc = 0;
   auto advance = [&]() {
     if (++sc == C) {
       sc = 0;
-      spair = next_visible(spair + 1);
+      scur = next_visible(step_cur(scur));
     }
   };
-  if (pair < np) {
-    const Pair r = pair_at(pair);
+  float lse_v = 0.f, del_v = 0.f;
+  if (cur.i < np) {
+    const Pair r = pair_of(cur);
+    rowstats(r, lse_v, del_v);
     stage_qo(r);
     for (int k = 0; k < RING - 1; ++k) {
-      stage_kv(k, spair < np ? pair_at(spair) : r, t0 * BN + (spair < np ? sc : 0) * BN);
+      stage_kv(k, scur.i < np ? pair_of(scur) : r, t0 * BN + (scur.i < np ? sc : 0) * BN);
       advance();
     }
   }
   vm_wait_all();
   __syncthreads();
-  while (pair < np) {
-    const Pair r = pair_at(pair);
-    const int nxt = next_visible(pair + 1);
+  while (cur.i < np) {
+    const Pair r = pair_of(cur);
+    const Cur nxc = next_visible(step_cur(cur));
+    const bool has_next = nxc.i < np;
     const int b = r.b, hq = r.hq, Lq = r.Lq, Lk = r.Lk;
     const bool qvalid = qi < Lq;
+    // this pair's LSE2 / -delta were loaded a step ago: landed before this step's LDS-DMA goes out
+    // (the compiler's own wait for them counts no LDS-DMA: waited at their use it would be a
+    // vmcnt(0) that drains this step's prefetches)
+    asm volatile("" : "+v"(lse_v), "+v"(del_v));
+    const float nlse = qvalid ? -lse_v : 0.f;
+    const float ndel = qvalid ? del_v : 0.f;  // the workspace holds -delta
+    // the next pair's go out ahead of this step's LDS-DMA, so the step-end wait retires them
+    // (loaded at the step start and waited at once, each step had exposed one load latency)
+    float lse_n = 0.f, del_n = 0.f;
+    if (has_next) rowstats(pair_of(nxc), lse_n, del_n);
     u32x4 qf[KS], of[KS];
     if constexpr (QLDS) {
 #pragma unroll
@@ -1364,19 +1475,11 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
         of[ks] = load_row_frag<ALIGNED>(orow, 16 * ks + 8 * hh, D, qvalid);
       }
     }
-    const int64_t srow = (int64_t)(b * p.heads_q + hq) * p.lse_row_stride;
-    // (unconditional loads, so that the step's VMEM count is fixed; row 0 exists: Lq > 0)
-    float lse_v = p.lse[srow + (qvalid ? qi : 0)], del_v = p.delta[srow + (qvalid ? qi : 0)];
-    // landed before this step's LDS-DMA goes out: the compiler's own wait for them counts no
-    // LDS-DMA, so waited at their use it would be a vmcnt(0) that drains this step's prefetches
-    asm volatile("" : "+v"(lse_v), "+v"(del_v));
-    const float nlse = qvalid ? -lse_v : 0.f;
-    const float ndel = qvalid ? del_v : 0.f;  // the workspace holds -delta
     if constexpr (QLDS) {
       // every wave holds its fragments: the next pair's rows may overwrite the tiles
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __syncthreads();
-      if (nxt < np) stage_qo(pair_at(nxt));
+      if (has_next) stage_qo(pair_of(nxc));
       else if (DEEP) stage_qo(r);  // (unused: keeps the step's load count)
     }
     const int lim_lane = !qvalid ? 0 : (CAUSAL ? min(Lk, qi + Lk - Lq + 1) : Lk);
@@ -1395,11 +1498,11 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
       if (RING == 3 || it < r.tend) {
         const int n0 = it * BN;
         if constexpr (RING == 3) {  // the tile RING - 1 steps ahead (every step of a pair runs)
-          stage_kv(buf == 0 ? 2 : buf - 1, spair < np ? pair_at(spair) : r, (t0 + (spair < np ? sc : 0)) * BN);
+          stage_kv(buf == 0 ? 2 : buf - 1, scur.i < np ? pair_of(scur) : r, (t0 + (scur.i < np ? sc : 0)) * BN);
           advance();
         } else {  // the next tile: this pair's, else the next visible pair's first
           if (it + 1 < r.tend) stage_kv(buf ^ 1, r, n0 + BN);
-          else if (nxt < np) stage_kv(buf ^ 1, pair_at(nxt), t0 * BN);
+          else if (has_next) stage_kv(buf ^ 1, pair_of(nxc), t0 * BN);
         }
         const char* K = kt(buf);
         const char* V = vt(buf);
@@ -1468,7 +1571,9 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
         buf = RING == 3 ? (buf == 2 ? 0 : buf + 1) : buf ^ 1;
       }
     }
-    pair = nxt;
+    cur = nxc;
+    lse_v = lse_n;
+    del_v = del_n;
   }
 
   // one store of the block (16-byte stores when the rows allow them: a group's 4 keys are contiguous)

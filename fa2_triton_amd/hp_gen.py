@@ -2055,7 +2055,7 @@ class DkdvGen:
         if self.dropout:
             e.salu("s_mov_b32 s84, %[mlo]")
             e.salu("s_mov_b32 s85, %[mhi]")
-            e.salu("s_mov_b32 s86, -1")
+            e.salu("s_mov_b32 s86, %[mrange]")  # the mask's bytes from the base: reads past it give 0
             e.salu("s_mov_b32 s87, 0x20000")
             # sb + w0 + 256 w (lbs = sb + rows)
             e.salu(f"s_lshl_b32 {D_WL}, %[w0], 8")
@@ -2180,7 +2180,7 @@ def gen_dkdv_function(bf16, causal, dropout=False):
     kops = ", ".join(f'[k{i}] "v"(kf[{i}])' for i in range(16))
     sops = ["ng", "nmt", "c0", "c01", "c012", "mlast", "lq", "qrb"] + ([] if dropout else ["orb"]) + ["qwrap",
             "owrap", "lwrap", "lc0", "qlo", "qhi", "olo", "ohi", "lselo", "lsehi", "dllo", "dlhi", "mlds", "lbs", "w0",
-            "sc"] + (["kd0"] if causal else []) + (["mlo", "mhi", "mstep", "mwrap"] if dropout else [])
+            "sc"] + (["kd0"] if causal else []) + (["mlo", "mhi", "mrange", "mstep", "mwrap"] if dropout else [])
     vops = ["qb0", "qb1", "vb0", "vb1", "ta", "tb"] + (["qb0h", "qb1h", "tah", "tbh"] if g.L.nbuf > 4 else []) + ["lb", "qoff0", "qoff1"] + ([] if dropout else ["ooff0", "ooff1"]) + \
         ["lsoff"] + (["lr"] if causal else []) + (["dscb"] if dropout else [])
     src = f"""// hand-placed dK/dV statement ({'bf16' if bf16 else 'fp16'}, {'causal' if causal else 'non-causal'}): {len(lines)} lines, {g.e.n_mfma} MFMAs
