@@ -1208,57 +1208,6 @@ FA2_DEV void dbias_block(int g, int nmb, int nkc, int& mb, int& kc) {
   if (c >= sqk || mb >= nmb || kc >= nkc) mb = -1;
 }
 
-// Causal: an XCD's visible blocks first, in the square order above, then its empty ones.  Under the
-// plain order the empty blocks (above the diagonal, gone in microseconds) sat among the visible
-// ones, so an XCD's workgroups started their blocks at scattered times and walked the pairs out of
-// step: the Q / dO and K / V rows one workgroup fetched for a pair had left the L2 before the
-// others sharing them reached that pair.  Visible first, the 32 workgroups an XCD runs at once
-// start together on neighbouring blocks and stay in step (equal work per block).  The order is a
-// speed choice only: every block still decides per pair what it sees (varlen included).
-// dbias_lim: the key chunks row block mb sees at the padded lengths (a prefix kc < lim)
-__host__ __device__ inline int dbias_lim(int mb, int nkc, int Lq, int Lk) {
-  if (mb * 128 >= Lq) return 0;
-  const int n_end = max(min(Lk, (mb + 1) * 128 + Lk - Lq), 0);
-  return min(nkc, (n_end + 64 * kDbiasChunk - 1) / (64 * kDbiasChunk));
-}
-__host__ __device__ inline void dbias_block_visible_first(int g, int nmb, int nkc, int Lq, int Lk, int& mb, int& kc) {
-  const int e = dbias_side(nmb, nkc);
-  const int x = g & 7, j = g >> 3;
-  const int sqr = (nmb + e - 1) / e, sqk = (nkc + e - 1) / e, per_row = (sqk + 7) / 8;
-  const int nsq = sqr * per_row;  // the XCD's squares q = r per_row + m, column c = ((x - r) & 7) + 8 m
-  // blocks of square q's row i: valid chunks [lo, hi), the visible ones a prefix of nv
-  auto row = [&](int q, int i, int& m_, int& lo, int& hi, int& nv) {
-    const int r = q / per_row, c = ((x - r) & 7) + 8 * (q - r * per_row);
-    m_ = r * e + i;
-    lo = c * e;
-    hi = (c < sqk && m_ < nmb) ? min(lo + e, nkc) : lo;
-    nv = min(max(dbias_lim(m_, nkc, Lq, Lk) - lo, 0), hi - lo);
-  };
-  int nvis = 0;
-  for (int q = 0; q < nsq; ++q)
-    for (int i = 0; i < e; ++i) {
-      int m_, lo, hi, nv;
-      row(q, i, m_, lo, hi, nv);
-      nvis += nv;
-    }
-  const bool vis = j < nvis;
-  int rem = vis ? j : j - nvis;
-  mb = -1;
-  kc = 0;
-  for (int q = 0; q < nsq; ++q)
-    for (int i = 0; i < e; ++i) {
-      int m_, lo, hi, nv;
-      row(q, i, m_, lo, hi, nv);
-      const int cnt = vis ? nv : hi - lo - nv;
-      if (rem < cnt) {
-        mb = m_;
-        kc = lo + (vis ? 0 : nv) + rem;
-        return;
-      }
-      rem -= cnt;
-    }
-}
-
 template <bool BF16, int DT, bool CAUSAL, bool DROPOUT, bool ALIGNED>
 __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kernel(const fa2_bwd_args p) {
   using E = Elem<BF16>;
@@ -1285,10 +1234,7 @@ __global__ void __launch_bounds__(256, DT <= 64 && !DROPOUT ? 2 : 1) dbias_kerne
   const int nkt = (p.seqlen_k + BN - 1) / BN;        // key tiles of the output rows
   const int nkc = (nkt + C - 1) / C;
   int mb, kc;
-  if (CAUSAL)
-    dbias_block_visible_first(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, p.seqlen_q, p.seqlen_k, mb, kc);
-  else
-    dbias_block(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, mb, kc);
+  dbias_block(blockIdx.x, (p.seqlen_q + BM - 1) / BM, nkc, mb, kc);
   if (mb < 0) return;                                // grid padding
   const int t0 = kc * C, t1 = min(nkt, t0 + C);     // this workgroup's key tiles
   const int Hb = p.bias_stride[1] != 0 ? p.heads_q : 1;
