@@ -195,6 +195,26 @@ def test_bias_gradient_kernels_have_no_scratch(kernels):
     assert not {k: v[0] for k, v in found.items() if v[0]}, "scratch bytes per lane"
 
 
+# the kernels a D = 128 run with a 16-bit bias whose rows are 16-byte aligned dispatches to (the
+# bench's --bias line; the reference's test_fwd_only always has a bias): the pipelined forward
+# and dK/dV spill nothing; the bias dQ spills a few dwords at two waves per SIMD (one wave per SIMD
+# removes it but measured 20 % slower), bounded here so that it cannot grow unnoticed
+BIAS_LINE = {
+    "fwd_pipe": (r"_ZN3fa215fwd_pipe_kernelILb[01]ELi128ELb[01]ELi4ELi1[67]EEEv12fa2_fwd_args", 0),
+    "dkdv": (r"_ZN3fa211dkdv_kernelILb[01]ELi128ELb[01]ELi1[67]ELb0ELb1EEEv12fa2_bwd_argsi", 0),
+    "dq": (r"_ZN3fa29dq_kernelILb[01]ELi128ELb[01]ELi1[67]ELb0ELb1ELb[01]EEEv12fa2_bwd_args", 48),
+}
+
+
+@pytest.mark.parametrize("kind", sorted(BIAS_LINE))
+def test_bias_line_kernels_scratch(kernels, kind):
+    pat, limit = BIAS_LINE[kind]
+    found = {k: v for k, v in kernels.items() if re.match(pat + "$", k)}
+    assert len(found) == (16 if kind == "dq" else 8), (kind, sorted(found))  # dtypes x causal x bias dtype (x dQ dtype)
+    over = {k: v[0] for k, v in found.items() if v[0] > limit}
+    assert not over, f"scratch bytes per lane over {limit}: {over}"
+
+
 # The next unit's Q (forward) and Q / dO (dQ) fragments are loaded by the main statement's tail
 # straight into its "+a" operand registers and stay in flight across the compiler's epilogue
 # code: nothing may read, copy or overwrite those AGPRs before the wait (the
